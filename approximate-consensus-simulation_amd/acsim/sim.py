@@ -1,0 +1,187 @@
+"""User-facing API: ``simulate(cfg)`` and ``Simulator(cfg).round(k)``.
+
+Thin ctypes layer over libacsim.so (include/acsim.h).  The per-round hot path runs in the
+library's HIP kernels; this module only marshals configs and host buffers.  There is no CPU
+fallback: ``backend="cpu"`` is rejected (the CPU spec reference is test infrastructure in
+oracle/, not part of the product).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _abi
+from .config import Config, preset
+
+
+@dataclass
+class RoundInfo:
+    round: int
+    done: bool
+    spread: float
+    lo: float
+    hi: float
+    instances_done: int
+
+
+@dataclass
+class Result:
+    rounds: np.ndarray          # uint32 [B]
+    converged: np.ndarray       # bool [B]
+    spread: np.ndarray          # float64 [B], final spread per instance
+    node_rounds: int
+    wall_seconds: float
+    rounds_max: int
+    x_final: Optional[np.ndarray] = None      # [N] for B == 1, [B, N] otherwise (if requested)
+    spread_trace: Optional[np.ndarray] = None  # instance 0, if cfg.trace_spread
+
+
+class Simulator:
+    """One device-resident simulation handle (``acs_sim``)."""
+
+    def __init__(self, cfg: Config | str, device: int = 0, backend: str = "hip"):
+        if isinstance(cfg, str):
+            cfg = preset(cfg)
+        if backend != "hip":
+            raise ValueError("acsim implements backend='hip' only; the CPU spec reference is "
+                             "test infrastructure (oracle/) and is not a product backend")
+        self.cfg = cfg
+        self._lib = _abi.load_library()
+        self._c = cfg.to_c()
+        devs = (C.c_int * 1)(int(device))
+        h = C.c_void_p()
+        _abi.check(self._lib, self._lib.acs_create(C.byref(self._c), _abi.BACKEND_HIP, devs, 1,
+                                                   C.byref(h)))
+        self._h = h
+
+    # -------------------------------------------------------------------------- lifecycle
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.acs_destroy(self._h)
+        self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, code: int) -> None:
+        _abi.check(self._lib, code)
+
+    @property
+    def N(self) -> int:
+        return int(self.cfg.n_nodes)
+
+    @property
+    def B(self) -> int:
+        return int(self.cfg.n_instances)
+
+    # -------------------------------------------------------------------------- stepping
+    def round(self, k: int = 1) -> RoundInfo:
+        """Advance every unfinished instance by at most k rounds (stops at convergence)."""
+        info = _abi.AcsRoundInfo()
+        self._chk(self._lib.acs_round(self._h, int(k), C.byref(info)))
+        return RoundInfo(info.round, bool(info.done), info.spread, info.lo, info.hi,
+                         info.instances_done)
+
+    def run(self) -> _abi.AcsResult:
+        res = _abi.AcsResult()
+        self._chk(self._lib.acs_run(self._h, C.byref(res)))
+        return res
+
+    def sync(self) -> None:
+        self._chk(self._lib.acs_sync(self._h))
+
+    # -------------------------------------------------------------------------- state access
+    def values(self, instance: int = 0) -> np.ndarray:
+        out = np.empty(self.N, dtype=np.float64)
+        self._chk(self._lib.acs_get_values(self._h, int(instance), out.ctypes.data, out.size))
+        return out
+
+    def all_values(self) -> np.ndarray:
+        return np.stack([self.values(b) for b in range(self.B)])
+
+    def rounds(self) -> np.ndarray:
+        out = np.empty(self.B, dtype=np.uint32)
+        self._chk(self._lib.acs_get_instance_rounds(
+            self._h, out.ctypes.data_as(C.POINTER(C.c_uint32)), out.size))
+        return out
+
+    def converged(self) -> np.ndarray:
+        out = np.empty(self.B, dtype=np.uint8)
+        self._chk(self._lib.acs_get_instance_converged(
+            self._h, out.ctypes.data_as(C.POINTER(C.c_uint8)), out.size))
+        return out.astype(bool)
+
+    def spread(self) -> np.ndarray:
+        out = np.empty(self.B, dtype=np.float64)
+        self._chk(self._lib.acs_get_instance_spread(
+            self._h, out.ctypes.data_as(C.POINTER(C.c_double)), out.size))
+        return out
+
+    def spread_trace(self, instance: int = 0) -> np.ndarray:
+        n = int(self.cfg.max_rounds) + 1
+        out = np.empty(n, dtype=np.float64)
+        got = C.c_uint64()
+        self._chk(self._lib.acs_get_spread_trace(
+            self._h, int(instance), out.ctypes.data_as(C.POINTER(C.c_double)), n, C.byref(got)))
+        return out[: got.value].copy()
+
+    def set_state(self, round: int, x: np.ndarray) -> None:
+        x = np.ascontiguousarray(x, dtype=np.float64).reshape(-1)
+        self._chk(self._lib.acs_set_state(self._h, int(round), x.ctypes.data, x.size))
+
+    def fault_status(self) -> np.ndarray:
+        out = np.empty(self.B * self.N, dtype=np.uint32)
+        self._chk(self._lib.acs_get_fault_status(
+            self._h, out.ctypes.data_as(C.POINTER(C.c_uint32)), out.size))
+        return out.reshape(self.B, self.N)
+
+    def neighbors(self) -> np.ndarray:
+        d = int(self.cfg.degree)
+        out = np.empty(self.N * d, dtype=np.uint32)
+        self._chk(self._lib.acs_get_neighbors(
+            self._h, out.ctypes.data_as(C.POINTER(C.c_uint32)), out.size))
+        return out.reshape(self.N, d)
+
+    # -------------------------------------------------------------------------- measurement
+    def set_kernel_timing(self, enable: bool) -> None:
+        self._chk(self._lib.acs_set_kernel_timing(self._h, 1 if enable else 0))
+
+    def kernel_timing(self):
+        """(total_ms, launches, kernel_name) of the round kernel since timing was enabled."""
+        ms = C.c_double()
+        n = C.c_uint64()
+        name = C.create_string_buffer(256)
+        self._chk(self._lib.acs_get_kernel_timing(self._h, C.byref(ms), C.byref(n), name, 256))
+        return ms.value, n.value, name.value.decode()
+
+
+def simulate(cfg: Config | str, backend: str = "hip", device: int = 0,
+             devices: Optional[Sequence[int]] = None, return_values: bool = True) -> Result:
+    """Run one configuration to termination and return its results."""
+    if devices is not None:
+        devices = list(devices)
+        if len(devices) != 1:
+            raise ValueError("simulate() drives one device per process; shard instances across "
+                             "processes with acsim.distributed (one rank per GPU)")
+        device = devices[0]
+    with Simulator(cfg, device=device, backend=backend) as sim:
+        res = sim.run()
+        x = None
+        if return_values:
+            x = sim.values(0) if sim.B == 1 else sim.all_values()
+        trace = sim.spread_trace(0) if sim.cfg.trace_spread else None
+        return Result(rounds=sim.rounds(), converged=sim.converged(), spread=sim.spread(),
+                      node_rounds=int(res.node_rounds), wall_seconds=float(res.wall_seconds),
+                      rounds_max=int(res.rounds_max), x_final=x, spread_trace=trace)

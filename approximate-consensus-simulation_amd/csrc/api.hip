@@ -1,0 +1,623 @@
+// api.hip — C ABI (include/acsim.h) over the HIP round engine: handle lifecycle, HBM buffer
+// ownership, kernel-path selection, the round-chunk loop with device-side early exit, and the
+// bench-time kernel event timing.  SURVEY §8(b) (C1/C9).
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <chrono>
+#include <string>
+#include <vector>
+
+#include "../../include/acsim.h"
+#include "engine.hpp"
+
+using namespace acs;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return fail(ACS_EDEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                        __FILE__, __LINE__);                                              \
+    } while (0)
+
+enum Path { PATH_REGULAR = 0, PATH_GENERIC = 1, PATH_BATCHED = 2 };
+
+struct acs_sim {
+    acs_config c{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint64_t N = 0, B = 0, m = 0;
+    uint32_t d = 0, dp = 0;
+    Path path = PATH_GENERIC;
+    bool clean = true;
+    MsgParams mp{};
+    double* x[2] = {nullptr, nullptr};
+    uint32_t* ell = nullptr;
+    uint32_t* status = nullptr;
+    InstState* st = nullptr;
+    double2* partial = nullptr;
+    uint32_t nblk = 0, nblk_init = 0;
+    uint32_t* n_done = nullptr;
+    double* trace = nullptr;
+    uint32_t* h_ndone = nullptr;   // pinned [2]
+    uint32_t round = 0;            // round of every unfinished instance
+    bool all_done = false;
+    // kernel timing (bench)
+    bool timing = false;
+    std::vector<hipEvent_t> ev;    // pairs (start, stop)
+    size_t ev_used = 0;
+    double timed_ms = 0.0;
+    uint64_t timed_launches = 0;
+    std::string kname;
+};
+
+// ------------------------------------------------------------------------- validation
+// §A.8 constraints (restated here independently of the oracle's copy).
+static int validate(const acs_config* c) {
+    if (!c) return fail(ACS_EINVAL, "null config");
+    if (c->struct_size != sizeof(acs_config))
+        return fail(ACS_EINVAL, "struct_size %u != %zu", c->struct_size, sizeof(acs_config));
+    if (c->n_nodes < 1 || c->n_nodes > 0x7FFFFFFFull) return fail(ACS_EINVAL, "n_nodes out of range");
+    if (c->n_instances < 1) return fail(ACS_EINVAL, "n_instances must be >= 1");
+    if (c->instance_offset + c->n_instances > 0x100000000ull)
+        return fail(ACS_EINVAL, "global instance ids must fit in u32");
+    uint64_t m, slots;
+    if (c->topology == ACS_TOPO_COMPLETE) {
+        m = c->n_nodes;
+        slots = c->n_nodes * c->n_nodes;
+    } else if (c->topology == ACS_TOPO_RANDOM_REGULAR) {
+        if (c->degree < 2 || (c->degree & 1u) || c->degree > 4096)
+            return fail(ACS_EINVAL, "degree must be even, in [2, 4096]");
+        m = (uint64_t)c->degree + 1;
+        slots = c->n_nodes * (uint64_t)c->degree;
+    } else {
+        return fail(ACS_EINVAL, "unknown topology %u", c->topology);
+    }
+    if (slots >= (1ull << 34)) return fail(ACS_EINVAL, "slot count must be < 2^34");
+    switch (c->rule) {
+        case ACS_RULE_AVERAGE:
+            if (c->trim != 0) return fail(ACS_EINVAL, "AVERAGE requires trim == 0");
+            break;
+        case ACS_RULE_TRIMMED_MEAN:
+        case ACS_RULE_MIDPOINT:
+            if (m <= 2ull * c->trim) return fail(ACS_EINVAL, "need m > 2t");
+            break;
+        case ACS_RULE_DLPSW_SELECT:
+            if (c->trim < 1 || m <= 2ull * c->trim) return fail(ACS_EINVAL, "DLPSW needs t >= 1, m > 2t");
+            break;
+        default:
+            return fail(ACS_EINVAL, "unknown rule %u", c->rule);
+    }
+    if (c->fault_model == ACS_FAULT_NONE) {
+        if (c->n_faulty != 0) return fail(ACS_EINVAL, "n_faulty must be 0 without a fault model");
+    } else if (c->fault_model == ACS_FAULT_CRASH || c->fault_model == ACS_FAULT_BYZANTINE) {
+        if ((uint64_t)c->n_faulty >= c->n_nodes) return fail(ACS_EINVAL, "n_faulty must be < n_nodes");
+    } else {
+        return fail(ACS_EINVAL, "unknown fault model %u", c->fault_model);
+    }
+    if (c->fault_model == ACS_FAULT_CRASH && (c->crash_window < 1 || c->crash_window > (1u << 30)))
+        return fail(ACS_EINVAL, "crash_window must be in [1, 2^30]");
+    if (c->fault_model == ACS_FAULT_BYZANTINE) {
+        if (c->byz_strategy > ACS_BYZ_CONSTANT) return fail(ACS_EINVAL, "unknown byz strategy");
+        if (!(fabs(c->byz_delta) <= 1e100) || !(fabs(c->byz_const) <= 1e100))
+            return fail(ACS_EINVAL, "byz_delta / byz_const must be finite, |.| <= 1e100");
+        if (c->byz_strategy == ACS_BYZ_RANDOM && slots > (1ull << 33))
+            return fail(ACS_EINVAL, "BYZ RANDOM needs slot count <= 2^33");
+    }
+    if (!(c->loss_p >= 0.0 && c->loss_p < 1.0)) return fail(ACS_EINVAL, "loss_p must be in [0,1)");
+    if (c->mask_group < 1) return fail(ACS_EINVAL, "mask_group must be >= 1");
+    if (!(c->eps >= 0.0 && c->eps <= 1e300)) return fail(ACS_EINVAL, "eps must be finite, >= 0");
+    if (c->termination > ACS_TERM_FIXED) return fail(ACS_EINVAL, "unknown termination");
+    if (c->dtype != ACS_F64) return fail(ACS_EUNSUPPORTED, "only ACS_F64 is implemented");
+    if (c->trace_spread && c->n_instances * ((uint64_t)c->max_rounds + 1) > (1ull << 28))
+        return fail(ACS_EINVAL, "spread trace too large (B*(max_rounds+1) > 2^28)");
+    return ACS_OK;
+}
+
+static uint32_t drop_threshold(double p) {
+    const double t = floor(p * 4294967296.0);   // §A.5, in fp64
+    if (t <= 0.0) return 0u;
+    if (t >= 4294967295.0) return 0xFFFFFFFFu;
+    return (uint32_t)t;
+}
+
+// ------------------------------------------------------------------------- internals
+static void release(acs_sim* s) {
+    if (!s) return;
+    (void)hipSetDevice(s->device);
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
+    (void)hipFree(s->x[0]);
+    (void)hipFree(s->x[1]);
+    (void)hipFree(s->ell);
+    (void)hipFree(s->status);
+    (void)hipFree(s->st);
+    (void)hipFree(s->partial);
+    (void)hipFree(s->n_done);
+    (void)hipFree(s->trace);
+    if (s->h_ndone) (void)hipHostFree(s->h_ndone);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    delete s;
+}
+
+static FinalizeArgs make_finalize(acs_sim* s, uint32_t r_next, uint32_t nblk, bool init) {
+    FinalizeArgs f{};
+    f.st = s->st;
+    f.partial = s->partial;
+    f.nblk = nblk;
+    f.r_next = r_next;
+    f.max_rounds = s->c.max_rounds;
+    f.term_eps = s->c.termination == ACS_TERM_EPS;
+    f.eps = s->c.eps;
+    f.trace = s->trace;
+    f.trace_stride = (uint64_t)s->c.max_rounds + 1;
+    f.n_done = s->n_done;
+    f.init_mode = init ? 1u : 0u;
+    return f;
+}
+
+// (Re)initialise the per-instance state from x[round & 1] (create and set_state).
+static int init_state(acs_sim* s, uint32_t round) {
+    HIP_TRY(hipMemsetAsync(s->n_done, 0, sizeof(uint32_t), s->stream));
+    HIP_TRY(launch_partials_from_x(s->x[round & 1u], s->status, s->B, s->N, s->partial, s->nblk_init, s->stream));
+    const FinalizeArgs f = make_finalize(s, round, s->nblk_init, true);
+    HIP_TRY(launch_finalize(f, s->B, s->stream));
+    HIP_TRY(hipMemcpyAsync(s->h_ndone, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    s->round = round;
+    s->all_done = s->h_ndone[0] == s->B;
+    return ACS_OK;
+}
+
+static hipEvent_t next_event(acs_sim* s) {
+    if (s->ev_used == s->ev.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        s->ev.push_back(e);
+    }
+    return s->ev[s->ev_used++];
+}
+
+static int harvest_timing(acs_sim* s) {
+    if (s->ev_used == 0) return ACS_OK;
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    for (size_t k = 0; k + 1 < s->ev_used; k += 2) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
+        s->timed_ms += ms;
+        s->timed_launches += 1;
+    }
+    s->ev_used = 0;
+    return ACS_OK;
+}
+
+static int enqueue_round(acs_sim* s, uint32_t r) {
+    RoundArgs a{};
+    a.xin = s->x[r & 1u];
+    a.xout = s->x[(r + 1) & 1u];
+    a.ell = s->ell;
+    a.status = s->status;
+    a.st = s->st;
+    a.partial = s->partial;
+    a.N = s->N;
+    a.m = (uint32_t)s->m;
+    a.d = s->d;
+    a.dp = s->dp;
+    a.topology = s->c.topology;
+    a.rule = s->c.rule;
+    a.trim = s->c.trim;
+    a.r = r;
+    a.nblk = s->nblk;
+    a.mp = s->mp;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (s->timing) {
+        if (s->ev_used + 2 > 4096) {
+            int rc = harvest_timing(s);
+            if (rc) return rc;
+        }
+        e0 = next_event(s);
+        e1 = next_event(s);
+        if (!e0 || !e1) return fail(ACS_EDEVICE, "hipEventCreate failed");
+        HIP_TRY(hipEventRecord(e0, s->stream));
+    }
+    if (s->path == PATH_REGULAR)
+        HIP_TRY(launch_round_regular(a, s->B, s->clean, s->stream));
+    else
+        HIP_TRY(launch_round_generic(a, s->B, s->stream));
+    if (s->timing) HIP_TRY(hipEventRecord(e1, s->stream));
+    const FinalizeArgs f = make_finalize(s, r + 1, s->nblk, false);
+    HIP_TRY(launch_finalize(f, s->B, s->stream));
+    return ACS_OK;
+}
+
+static int read_states(acs_sim* s, std::vector<InstState>& out) {
+    out.resize(s->B);
+    HIP_TRY(hipMemcpyAsync(out.data(), s->st, s->B * sizeof(InstState), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return ACS_OK;
+}
+
+static constexpr uint32_t kChunk = 16;
+
+// Advance every unfinished instance by at most k rounds.
+static int advance(acs_sim* s, uint32_t k) {
+    if (s->all_done || k == 0) return ACS_OK;
+    const uint32_t cap = s->c.max_rounds > s->round ? s->c.max_rounds - s->round : 0;
+    if (k > cap) k = cap;
+    if (k == 0) return ACS_OK;
+    if (s->path == PATH_BATCHED) {
+        BatchArgs a{};
+        a.x0 = s->x[0];
+        a.x1 = s->x[1];
+        a.status = s->status;
+        a.st = s->st;
+        a.trace = s->trace;
+        a.trace_stride = (uint64_t)s->c.max_rounds + 1;
+        a.n_done = s->n_done;
+        a.N = (uint32_t)s->N;
+        a.rule = s->c.rule;
+        a.trim = s->c.trim;
+        a.max_rounds = s->c.max_rounds;
+        a.term_eps = s->c.termination == ACS_TERM_EPS;
+        a.eps = s->c.eps;
+        a.mp = s->mp;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (s->timing) {
+            e0 = next_event(s);
+            e1 = next_event(s);
+            if (!e0 || !e1) return fail(ACS_EDEVICE, "hipEventCreate failed");
+            HIP_TRY(hipEventRecord(e0, s->stream));
+        }
+        HIP_TRY(launch_batched_small(a, s->B, k, s->stream));
+        if (s->timing) HIP_TRY(hipEventRecord(e1, s->stream));
+        HIP_TRY(hipMemcpyAsync(s->h_ndone, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        s->round += k;
+        s->all_done = s->h_ndone[0] == s->B;
+        return ACS_OK;
+    }
+    const bool eps_mode = s->c.termination == ACS_TERM_EPS;
+    int slot = 0, prev = -1;
+    hipEvent_t poll[2] = {nullptr, nullptr};
+    while (k > 0 && !s->all_done) {
+        const uint32_t chunk = k < kChunk ? k : kChunk;
+        for (uint32_t q = 0; q < chunk; ++q) {
+            int rc = enqueue_round(s, s->round + q);
+            if (rc) return rc;
+        }
+        s->round += chunk;
+        k -= chunk;
+        if (s->round >= s->c.max_rounds) break;
+        if (eps_mode) {
+            // keep one chunk in flight: poll the previous chunk's done counter
+            HIP_TRY(hipMemcpyAsync(s->h_ndone + slot, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                   s->stream));
+            if (!poll[slot]) HIP_TRY(hipEventCreateWithFlags(&poll[slot], hipEventDisableTiming));
+            HIP_TRY(hipEventRecord(poll[slot], s->stream));
+            if (prev >= 0) {
+                HIP_TRY(hipEventSynchronize(poll[prev]));
+                if (s->h_ndone[prev] == s->B) s->all_done = true;
+            }
+            prev = slot;
+            slot ^= 1;
+        }
+    }
+    for (hipEvent_t e : poll)
+        if (e) (void)hipEventDestroy(e);
+    HIP_TRY(hipMemcpyAsync(s->h_ndone, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    s->all_done = s->h_ndone[0] == s->B;
+    return ACS_OK;
+}
+
+// ------------------------------------------------------------------------- C ABI
+extern "C" {
+
+int acs_abi_version(void) { return ACS_ABI_VERSION; }
+
+const char* acs_last_error(void) { return g_err.c_str(); }
+
+int acs_create(const acs_config* cfg, int backend, const int* devices, int n_devices, acs_sim** out) {
+    if (!out) return fail(ACS_EINVAL, "null out");
+    *out = nullptr;
+    int rc = validate(cfg);
+    if (rc) return rc;
+    if (backend != ACS_HIP)
+        return fail(ACS_EUNSUPPORTED, "libacsim implements ACS_HIP only (the CPU spec reference is the "
+                                      "test oracle in oracle/, not a product backend)");
+    if (n_devices != 1 || !devices)
+        return fail(ACS_EINVAL, "exactly one device per handle (shard across processes, one rank per GPU)");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(ACS_EDEVICE, "no HIP device");
+    if (devices[0] < 0 || devices[0] >= ndev) return fail(ACS_EINVAL, "device %d out of range", devices[0]);
+
+    acs_sim* s = new acs_sim();
+    s->c = *cfg;
+    s->device = devices[0];
+    s->N = cfg->n_nodes;
+    s->B = cfg->n_instances;
+    s->m = cfg->topology == ACS_TOPO_COMPLETE ? s->N : (uint64_t)cfg->degree + 1;
+    s->d = cfg->degree;
+    s->dp = (cfg->degree + 3u) & ~3u;
+    s->clean = cfg->fault_model == ACS_FAULT_NONE && drop_threshold(cfg->loss_p) == 0;
+    s->mp.key = key_of(cfg->seed);
+    s->mp.thr = drop_threshold(cfg->loss_p);
+    s->mp.fault = cfg->fault_model;
+    s->mp.byz = cfg->byz_strategy;
+    s->mp.mask_group = cfg->mask_group;
+    s->mp.inst_offset = cfg->instance_offset;
+    s->mp.delta = cfg->byz_delta;
+    s->mp.bconst = cfg->byz_const + 0.0;   // canonicalise -0.0 (no -0 ever enters a sort)
+
+    if (cfg->topology == ACS_TOPO_COMPLETE && s->N <= kBatchedMaxN) {
+        s->path = PATH_BATCHED;
+        s->kname = batched_small_name((uint32_t)s->N, cfg->rule);
+    } else if (cfg->topology == ACS_TOPO_RANDOM_REGULAR && regular_fast_supported(s->d, cfg->trim, cfg->rule)) {
+        s->path = PATH_REGULAR;
+        s->kname = regular_fast_name(s->d, cfg->trim, s->clean);
+    } else if (s->m <= kGenericMaxM) {
+        s->path = PATH_GENERIC;
+        s->kname = "k_round_generic";
+    } else {
+        delete s;
+        return fail(ACS_EUNSUPPORTED, "m = %llu entries per receiver exceeds the generic kernel's %u",
+                    (unsigned long long)(cfg->topology == ACS_TOPO_COMPLETE ? cfg->n_nodes : cfg->degree + 1ull),
+                    kGenericMaxM);
+    }
+    if (cfg->fault_model != ACS_FAULT_NONE && s->B * s->N >= (1ull << 31)) {
+        delete s;
+        return fail(ACS_EUNSUPPORTED, "fault schedules need B*N < 2^31");
+    }
+    s->nblk = s->path == PATH_REGULAR ? (uint32_t)((s->N + kRegularBlock - 1) / kRegularBlock)
+                                      : (s->path == PATH_GENERIC ? (uint32_t)s->N : 0u);
+    s->nblk_init = (uint32_t)((s->N + 255) / 256);
+    if (s->nblk_init > 1024) s->nblk_init = 1024;
+    const uint32_t ncap = s->nblk > s->nblk_init ? s->nblk : s->nblk_init;
+
+#define CREATE_TRY(expr)                                                                      \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) {                                                               \
+            int code_ = (e_ == hipErrorOutOfMemory || e_ == hipErrorMemoryAllocation) ? ACS_ENOMEM \
+                                                                                      : ACS_EDEVICE; \
+            fail(code_, "%s failed: %s", #expr, hipGetErrorString(e_));                       \
+            release(s);                                                                       \
+            return code_;                                                                     \
+        }                                                                                     \
+    } while (0)
+
+    CREATE_TRY(hipSetDevice(s->device));
+    CREATE_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    const uint64_t BN = s->B * s->N;
+    CREATE_TRY(hipMalloc(&s->x[0], BN * sizeof(double)));
+    CREATE_TRY(hipMalloc(&s->x[1], BN * sizeof(double)));
+    CREATE_TRY(hipMalloc(&s->st, s->B * sizeof(InstState)));
+    CREATE_TRY(hipMemsetAsync(s->st, 0, s->B * sizeof(InstState), s->stream));
+    CREATE_TRY(hipMalloc(&s->partial, s->B * (uint64_t)ncap * sizeof(double2)));
+    CREATE_TRY(hipMalloc(&s->n_done, sizeof(uint32_t)));
+    CREATE_TRY(hipHostMalloc(&s->h_ndone, 2 * sizeof(uint32_t), hipHostMallocDefault));
+    if (cfg->trace_spread) {
+        const uint64_t nt = s->B * ((uint64_t)cfg->max_rounds + 1);
+        CREATE_TRY(hipMalloc(&s->trace, nt * sizeof(double)));
+        CREATE_TRY(hipMemsetAsync(s->trace, 0xFF, nt * sizeof(double), s->stream));   // NaN
+    }
+    if (cfg->topology == ACS_TOPO_RANDOM_REGULAR) {
+        const uint64_t words = ((s->N + 63) / 64) * 64ull * s->dp;
+        CREATE_TRY(hipMalloc(&s->ell, words * sizeof(uint32_t)));
+        CREATE_TRY(hipMemsetAsync(s->ell, 0, words * sizeof(uint32_t), s->stream));
+        const uint64_t gseed = cfg->graph_seed ? cfg->graph_seed : cfg->seed;
+        CREATE_TRY(launch_build_ell(s->ell, s->N, s->d, s->dp, make_feistel(s->N, gseed), s->stream));
+    }
+    if (cfg->fault_model != ACS_FAULT_NONE) {
+        CREATE_TRY(hipMalloc(&s->status, BN * sizeof(uint32_t)));
+        CREATE_TRY(build_fault_status(s->status, s->B, s->N, cfg->n_faulty, cfg->fault_model,
+                                      cfg->crash_window, s->mp.key, cfg->instance_offset, s->stream));
+    }
+    CREATE_TRY(launch_init_values(s->x[0], s->B, s->N, s->mp.key, cfg->instance_offset, s->stream));
+#undef CREATE_TRY
+    rc = init_state(s, 0);
+    if (rc) {
+        release(s);
+        return rc;
+    }
+    *out = s;
+    return ACS_OK;
+}
+
+void acs_destroy(acs_sim* s) { release(s); }
+
+static void fill_info(acs_sim* s, const std::vector<InstState>& v, acs_round_info* out) {
+    if (!out) return;
+    memset(out, 0, sizeof *out);
+    uint64_t nd = 0;
+    double sp = -INFINITY;
+    uint32_t rmax = 0;
+    for (const InstState& e : v) {
+        nd += e.done;
+        if (e.spread > sp) sp = e.spread;
+        if (e.rounds > rmax) rmax = e.rounds;
+    }
+    out->round = rmax;
+    out->done = nd == v.size();
+    out->spread = sp;
+    out->lo = v[0].lo;
+    out->hi = v[0].hi;
+    out->instances_done = nd;
+}
+
+int acs_round(acs_sim* s, uint32_t k, acs_round_info* out) {
+    if (!s) return fail(ACS_EINVAL, "null sim");
+    HIP_TRY(hipSetDevice(s->device));
+    int rc = advance(s, k);
+    if (rc) return rc;
+    std::vector<InstState> v;
+    rc = read_states(s, v);
+    if (rc) return rc;
+    fill_info(s, v, out);
+    return ACS_OK;
+}
+
+int acs_run(acs_sim* s, acs_result* out) {
+    if (!s) return fail(ACS_EINVAL, "null sim");
+    HIP_TRY(hipSetDevice(s->device));
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc = advance(s, s->c.max_rounds);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    const auto t1 = std::chrono::steady_clock::now();
+    std::vector<InstState> v;
+    rc = read_states(s, v);
+    if (rc) return rc;
+    if (out) {
+        memset(out, 0, sizeof *out);
+        out->n_instances = s->B;
+        out->final_spread_max = -INFINITY;
+        for (const InstState& e : v) {
+            if (e.rounds > out->rounds_max) out->rounds_max = e.rounds;
+            out->n_converged += e.converged;
+            out->node_rounds += s->N * (uint64_t)e.rounds;
+            if (e.spread > out->final_spread_max) out->final_spread_max = e.spread;
+        }
+        out->wall_seconds = std::chrono::duration<double>(t1 - t0).count();
+    }
+    return ACS_OK;
+}
+
+int acs_sync(acs_sim* s) {
+    if (!s) return fail(ACS_EINVAL, "null sim");
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return ACS_OK;
+}
+
+int acs_get_values(acs_sim* s, uint64_t b, void* out, uint64_t n) {
+    if (!s || !out || b >= s->B || n < s->N) return fail(ACS_EINVAL, "bad get_values arguments");
+    HIP_TRY(hipSetDevice(s->device));
+    InstState e;
+    HIP_TRY(hipMemcpyAsync(&e, s->st + b, sizeof e, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    HIP_TRY(hipMemcpyAsync(out, s->x[e.rounds & 1u] + b * s->N, s->N * sizeof(double), hipMemcpyDeviceToHost,
+                           s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return ACS_OK;
+}
+
+int acs_get_instance_rounds(acs_sim* s, uint32_t* out, uint64_t n) {
+    if (!s || !out || n < s->B) return fail(ACS_EINVAL, "bad arguments");
+    std::vector<InstState> v;
+    int rc = read_states(s, v);
+    if (rc) return rc;
+    for (uint64_t b = 0; b < s->B; ++b) out[b] = v[b].rounds;
+    return ACS_OK;
+}
+
+int acs_get_instance_converged(acs_sim* s, uint8_t* out, uint64_t n) {
+    if (!s || !out || n < s->B) return fail(ACS_EINVAL, "bad arguments");
+    std::vector<InstState> v;
+    int rc = read_states(s, v);
+    if (rc) return rc;
+    for (uint64_t b = 0; b < s->B; ++b) out[b] = (uint8_t)v[b].converged;
+    return ACS_OK;
+}
+
+int acs_get_instance_spread(acs_sim* s, double* out, uint64_t n) {
+    if (!s || !out || n < s->B) return fail(ACS_EINVAL, "bad arguments");
+    std::vector<InstState> v;
+    int rc = read_states(s, v);
+    if (rc) return rc;
+    for (uint64_t b = 0; b < s->B; ++b) out[b] = v[b].spread;
+    return ACS_OK;
+}
+
+int acs_get_spread_trace(acs_sim* s, uint64_t b, double* out, uint64_t n, uint64_t* n_out) {
+    if (!s || !out || b >= s->B) return fail(ACS_EINVAL, "bad arguments");
+    if (!s->trace) return fail(ACS_EINVAL, "trace_spread was not enabled");
+    InstState e;
+    HIP_TRY(hipMemcpyAsync(&e, s->st + b, sizeof e, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    uint64_t cnt = (uint64_t)e.rounds + 1;
+    if (cnt > n) cnt = n;
+    HIP_TRY(hipMemcpyAsync(out, s->trace + b * ((uint64_t)s->c.max_rounds + 1), cnt * sizeof(double),
+                           hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    if (n_out) *n_out = cnt;
+    return ACS_OK;
+}
+
+int acs_set_state(acs_sim* s, uint32_t round, const void* x, uint64_t n) {
+    if (!s || !x || n != s->B * s->N) return fail(ACS_EINVAL, "set_state needs B*N values");
+    if (round > s->c.max_rounds) return fail(ACS_EINVAL, "round > max_rounds");
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipMemcpyAsync(s->x[round & 1u], x, n * sizeof(double), hipMemcpyHostToDevice, s->stream));
+    return init_state(s, round);
+}
+
+int acs_get_fault_status(acs_sim* s, uint32_t* out, uint64_t n) {
+    if (!s || !out || n < s->B * s->N) return fail(ACS_EINVAL, "bad arguments");
+    HIP_TRY(hipSetDevice(s->device));
+    if (!s->status) {
+        for (uint64_t k = 0; k < s->B * s->N; ++k) out[k] = kHonest;
+        return ACS_OK;
+    }
+    HIP_TRY(hipMemcpyAsync(out, s->status, s->B * s->N * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return ACS_OK;
+}
+
+int acs_get_neighbors(acs_sim* s, uint32_t* out, uint64_t n) {
+    if (!s || !out) return fail(ACS_EINVAL, "bad arguments");
+    if (!s->ell) return fail(ACS_EINVAL, "not a RANDOM_REGULAR topology");
+    if (n < s->N * s->d) return fail(ACS_EINVAL, "buffer too small");
+    HIP_TRY(hipSetDevice(s->device));
+    const uint64_t words = ((s->N + 63) / 64) * 64ull * s->dp;
+    std::vector<uint32_t> h(words);
+    HIP_TRY(hipMemcpyAsync(h.data(), s->ell, words * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    for (uint64_t i = 0; i < s->N; ++i)
+        for (uint32_t t = 0; t < s->d; ++t)
+            out[i * s->d + t] = h[(((i >> 6) * (s->dp >> 2) + (t >> 2)) * 64 + (i & 63)) * 4 + (t & 3)];
+    return ACS_OK;
+}
+
+int acs_set_kernel_timing(acs_sim* s, int enable) {
+    if (!s) return fail(ACS_EINVAL, "null sim");
+    HIP_TRY(hipSetDevice(s->device));
+    int rc = harvest_timing(s);
+    if (rc) return rc;
+    s->timing = enable != 0;
+    s->timed_ms = 0.0;
+    s->timed_launches = 0;
+    return ACS_OK;
+}
+
+int acs_get_kernel_timing(acs_sim* s, double* total_ms, uint64_t* launches, char* kernel_name,
+                          uint64_t name_cap) {
+    if (!s) return fail(ACS_EINVAL, "null sim");
+    HIP_TRY(hipSetDevice(s->device));
+    int rc = harvest_timing(s);
+    if (rc) return rc;
+    if (total_ms) *total_ms = s->timed_ms;
+    if (launches) *launches = s->timed_launches;
+    if (kernel_name && name_cap) {
+        strncpy(kernel_name, s->kname.c_str(), name_cap - 1);
+        kernel_name[name_cap - 1] = 0;
+    }
+    return ACS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,216 @@
+// batched_small.hip — persistent batched kernel for COMPLETE graphs with N <= 64 (cfg1, cfg3).
+//
+// One wavefront = one instance, lane i = node i.  x stays in a VGPR across rounds; a sender's
+// value reaches every receiver with v_readlane (compile-time lane index -> SGPR broadcast), so a
+// round touches no memory at all.  Per lane and round:
+//   - the §A.5 drop mask of its N slots (one Philox call per 4 slots) and §A.4 crash bits;
+//   - AVERAGE (cfg3): the §A.7 tree sum over entries in entry order, evaluated as an adjacent-
+//     pair stack over the bit-reversed entry sequence (stride-halving over a[] == adjacent
+//     pairing over a[bitrev(k)]; fp add is commutative, so the sum is bit-identical), using
+//     log2(P) registers instead of P;
+//   - sorting rules (cfg1 MIDPOINT): a compile-time P-wire network in registers, then the
+//     runtime-t window read back from a lane-private LDS column;
+//   - honest (min, max) by wavefront shuffles, ε test, early exit per instance (§A.8).
+// HBM traffic: 8N bytes in and out per instance per launch.  Bound: integer VALU (Philox).
+#include "resolve.hpp"
+#include "sortnet.hpp"
+
+namespace acs {
+
+template <int L>
+constexpr int bitrev(int q) {
+    int r = 0;
+    for (int b = 0; b < L; ++b)
+        if (q & (1 << b)) r |= 1 << (L - 1 - b);
+    return r;
+}
+
+constexpr int ilog2(int p) {
+    int l = 0;
+    while ((1 << l) < p) ++l;
+    return l;
+}
+
+template <int P, int Q, int LOG2P>
+__device__ __forceinline__ void push_leaf(double (&acc)[LOG2P + 1], double v) {
+    // combine while bit l of Q is set (compile-time), then park at level l
+    if constexpr ((Q & 1) && LOG2P > 0) {
+        v = acc[0] + v;
+        if constexpr ((Q & 2) && LOG2P > 1) {
+            v = acc[1] + v;
+            if constexpr ((Q & 4) && LOG2P > 2) {
+                v = acc[2] + v;
+                if constexpr ((Q & 8) && LOG2P > 3) {
+                    v = acc[3] + v;
+                    if constexpr ((Q & 16) && LOG2P > 4) {
+                        v = acc[4] + v;
+                        if constexpr ((Q & 32) && LOG2P > 5) {
+                            v = acc[5] + v;
+                            acc[6] = v;
+                        } else acc[5] = v;
+                    } else acc[4] = v;
+                } else acc[3] = v;
+            } else acc[2] = v;
+        } else acc[1] = v;
+    } else {
+        acc[0] = v;
+    }
+}
+
+struct LaneCtx {
+    const MsgParams* mp;
+    uint32_t N, lane, b, r;
+    double xi, lo, hi;
+    uint32_t sti;
+    uint64_t miss;   // bit j: message from j missing (crash or drop)
+};
+
+// §A.6 entry j of receiver `lane` (valid for j < N)
+__device__ __forceinline__ double entry_value(const LaneCtx& c, int j) {
+    const double xj = readlane_f64(c.xi, j);
+    const uint32_t stj = (uint32_t)__builtin_amdgcn_readlane((int)c.sti, j);
+    if ((uint32_t)j == c.lane) return c.xi;
+    if ((c.miss >> j) & 1ull) return c.xi;
+    if (stj == kByz) return byz_value(*c.mp, c.b, c.r, c.lane, (uint64_t)c.lane * c.N + j, c.lo, c.hi);
+    return xj;
+}
+
+template <int P, int... Q>
+__device__ __forceinline__ double average_tree(const LaneCtx& c, std::integer_sequence<int, Q...>) {
+    constexpr int LOG2P = ilog2(P);
+    double acc[LOG2P + 1];
+    (push_leaf<P, Q, LOG2P>(acc, (bitrev<LOG2P>(Q) < (int)c.N) ? entry_value(c, bitrev<LOG2P>(Q)) : 0.0), ...);
+    return acc[LOG2P];
+}
+
+template <int P, bool SORT>
+__global__ __launch_bounds__(64) void k_batched_small(const BatchArgs a, uint32_t kmax) {
+    const uint32_t lb = blockIdx.x;
+    const uint32_t lane = threadIdx.x;
+    InstState* S = a.st + lb;
+    if (S->done) return;
+    const uint32_t N = a.N;
+    const MsgParams& mp = a.mp;
+    uint32_t r = S->rounds;
+    double lo = S->lo, hi = S->hi, spread = S->spread;
+    const uint32_t b = (uint32_t)(mp.inst_offset + lb);
+    const uint32_t bG = b - b % mp.mask_group;
+    const bool valid = lane < N;
+    const double* xin = ((r & 1u) ? a.x1 : a.x0) + (uint64_t)lb * N;
+    double xi = valid ? xin[lane] : 0.0;
+    const uint32_t sti = valid ? (a.status ? a.status[(uint64_t)lb * N + lane] : kHonest) : kByz;
+    const bool honest = sti == kHonest;
+    __shared__ double colbuf[SORT ? P * 64 : 1];
+    bool done = false, conv = spread <= a.eps;
+    for (uint32_t q = 0; q < kmax; ++q) {
+        const bool act = valid && is_active(sti, r);
+        LaneCtx c;
+        c.mp = &mp; c.N = N; c.lane = lane; c.b = b; c.r = r; c.xi = xi; c.lo = lo; c.hi = hi;
+        c.sti = sti;
+        c.miss = 0;
+        // drop mask (§A.5): slot s = lane*N + j
+        if (mp.thr && act) {
+            if ((N & 3u) == 0) {
+                const uint32_t nq = N >> 2;
+                for (uint32_t g = 0; g < nq; ++g) {
+                    const U4 w = philox10(lane * nq + g, r, bG, kStreamDrop, mp.key);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (w.v[e] < mp.thr) c.miss |= 1ull << (4 * g + e);
+                }
+            } else {
+                for (uint32_t j = 0; j < N; ++j)
+                    if (draw(mp.key, kStreamDrop, bG, r, (uint64_t)lane * N + j) < mp.thr) c.miss |= 1ull << j;
+            }
+        }
+        // crash bits (§A.4): sender status is uniform per j
+        if (mp.fault == 1 && act) {
+            for (uint32_t j = 0; j < N; ++j) {
+                const uint32_t stj = (uint32_t)__builtin_amdgcn_readlane((int)sti, (int)j);
+                if (stj < kByz && r >= stj && crash_missing(mp, stj, b, r, (uint64_t)lane * N + j))
+                    c.miss |= 1ull << j;
+            }
+        }
+        double res;
+        if constexpr (!SORT) {
+            res = average_tree<P>(c, std::make_integer_sequence<int, P>{}) / (double)N;
+        } else {
+            double v[P];
+#pragma unroll
+            for (int j = 0; j < P; ++j) v[j] = j < (int)N ? entry_value(c, j) : kInf;
+            select_sort<P>(v);
+#pragma unroll
+            for (int k = 0; k < P; ++k) colbuf[k * 64 + lane] = v[k];
+            const uint32_t t = a.trim, nr = N - 2 * t;
+            if (a.rule == 2) {
+                res = (colbuf[t * 64 + lane] + colbuf[(N - t - 1) * 64 + lane]) * 0.5;
+            } else {
+                const uint32_t step = a.rule == 3 ? t : 1;
+                const uint32_t cnt = a.rule == 3 ? (nr + t - 1) / t : nr;
+                uint32_t P2 = 1;
+                while (P2 < cnt) P2 <<= 1;
+                for (uint32_t k = 0; k < P2; ++k)   // in place: source index t + k*step >= k
+                    colbuf[k * 64 + lane] = k < cnt ? colbuf[(t + k * step) * 64 + lane] : 0.0;
+                for (uint32_t s2 = P2 >> 1; s2 >= 1; s2 >>= 1)
+                    for (uint32_t k = 0; k < s2; ++k)
+                        colbuf[k * 64 + lane] = colbuf[k * 64 + lane] + colbuf[(k + s2) * 64 + lane];
+                res = colbuf[lane] / (double)cnt;
+            }
+        }
+        xi = act ? res : xi;
+        r += 1;
+        lo = wave_min(honest ? xi : kInf);
+        hi = wave_max(honest ? xi : -kInf);
+        spread = hi - lo;
+        if (a.trace && lane == 0) a.trace[(uint64_t)lb * a.trace_stride + r] = spread;
+        conv = spread <= a.eps;
+        done = (a.term_eps && conv) || r >= a.max_rounds;
+        if (done) break;
+    }
+    double* xout = ((r & 1u) ? a.x1 : a.x0) + (uint64_t)lb * N;
+    if (valid) xout[lane] = xi;
+    if (lane == 0) {
+        S->lo = lo;
+        S->hi = hi;
+        S->spread = spread;
+        S->rounds = r;
+        S->converged = conv ? 1u : 0u;
+        S->done = done ? 1u : 0u;
+        if (done) atomicAdd(a.n_done, 1u);
+    }
+}
+
+static int pick_p(uint32_t N) {
+    int P = 2;
+    while ((uint32_t)P < N) P <<= 1;
+    return P;
+}
+
+const char* batched_small_name(uint32_t N, uint32_t rule) {
+    static const char* names[2][6] = {
+        {"k_batched_small<2,avg>", "k_batched_small<4,avg>", "k_batched_small<8,avg>",
+         "k_batched_small<16,avg>", "k_batched_small<32,avg>", "k_batched_small<64,avg>"},
+        {"k_batched_small<2,sort>", "k_batched_small<4,sort>", "k_batched_small<8,sort>",
+         "k_batched_small<16,sort>", "k_batched_small<32,sort>", "k_batched_small<64,sort>"}};
+    return names[rule != 0][ilog2(pick_p(N)) - 1];
+}
+
+hipError_t launch_batched_small(const BatchArgs& a, uint64_t B, uint32_t k, hipStream_t s) {
+    if (a.N < 1 || a.N > kBatchedMaxN) return hipErrorNotSupported;
+    const int P = pick_p(a.N);
+    const bool sort = a.rule != 0;
+    const dim3 grid((unsigned)B), block(64);
+#define L(PP)                                                                              \
+    case PP:                                                                               \
+        if (sort) hipLaunchKernelGGL((k_batched_small<PP, true>), grid, block, 0, s, a, k);  \
+        else hipLaunchKernelGGL((k_batched_small<PP, false>), grid, block, 0, s, a, k);     \
+        break;
+    switch (P) {
+        L(2) L(4) L(8) L(16) L(32) L(64)
+        default: return hipErrorNotSupported;
+    }
+#undef L
+    return hipGetLastError();
+}
+
+}  // namespace acs

@@ -1,0 +1,106 @@
+// engine.hpp — device-resident state and kernel launch interface of the round engine.
+//
+// HBM layout (per handle, one GPU):
+//   x[2]      : two fp64 buffers [B][N]; instance b at round r lives in x[r & 1] (Jacobi
+//               double buffer, never read and written in the same launch)
+//   ell       : RANDOM_REGULAR adjacency as column-major 64-row slices of 4-wide column
+//               groups, u32 [ceil(N/64)][Dp/4][64][4] (Dp = d rounded up to 4): lane l of a
+//               wave loads its 4 neighbour ids of group q with one 16-byte load, and the wave's
+//               64 loads are one contiguous 1 KiB line run
+//   status    : u32 [B][N] fault status (§A.4), absent when there are no faults
+//   st        : InstState [B] — honest lo/hi/spread of the current round, rounds, done flags
+//   partial   : double2 [B][nblk] per-block honest (min, max) partials of x^{r+1} (§A.8)
+//   trace     : f64 [B][max_rounds+1] optional spread trace
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "spec.hpp"
+
+namespace acs {
+
+struct InstState {
+    double lo, hi, spread;  // honest min / max / spread of the current x (§A.8)
+    uint32_t rounds;        // rounds executed
+    uint32_t done;          // terminated
+    uint32_t converged;     // spread <= eps
+    uint32_t pad;
+};
+
+struct RoundArgs {
+    const double* xin;        // x^r, instance-major [B][N]
+    double* xout;             // x^{r+1}
+    const uint32_t* ell;      // RANDOM_REGULAR adjacency (see layout above)
+    const uint32_t* status;   // [B][N] or nullptr when there are no faults
+    InstState* st;            // [B]
+    double2* partial;         // [B][nblk]
+    uint64_t N;
+    uint32_t m;               // entries per receiver
+    uint32_t d, dp;           // degree, degree rounded up to 4
+    uint32_t topology, rule, trim;
+    uint32_t r;               // round being produced: x^r -> x^{r+1}
+    uint32_t nblk;            // partial blocks per instance
+    MsgParams mp;
+};
+
+struct FinalizeArgs {
+    InstState* st;
+    const double2* partial;
+    uint32_t nblk;
+    uint32_t r_next;          // rounds value after this step (or the resumed round in init mode)
+    uint32_t max_rounds;
+    uint32_t term_eps;        // 1: EPS termination
+    double eps;
+    double* trace;            // nullptr if disabled
+    uint64_t trace_stride;    // max_rounds + 1
+    uint32_t* n_done;
+    uint32_t init_mode;       // 1: (re)initialisation, ignores the done flag
+};
+
+struct BatchArgs {
+    double* x0;               // buffer 0 [B][N]
+    double* x1;               // buffer 1 [B][N]
+    const uint32_t* status;   // [B][N] or nullptr
+    InstState* st;
+    double* trace;
+    uint64_t trace_stride;
+    uint32_t* n_done;
+    uint32_t N, rule, trim, max_rounds, term_eps;
+    double eps;
+    MsgParams mp;
+};
+
+// ---- setup kernels (setup.hip)
+hipError_t launch_init_values(double* x, uint64_t B, uint64_t N, Key key, uint64_t inst_offset,
+                              hipStream_t s);
+hipError_t launch_build_ell(uint32_t* ell, uint64_t N, uint32_t d, uint32_t dp, const Feistel& f,
+                            hipStream_t s);
+hipError_t build_fault_status(uint32_t* status, uint64_t B, uint64_t N, uint32_t f,
+                              uint32_t fault_model, uint32_t crash_window, Key key,
+                              uint64_t inst_offset, hipStream_t s);
+
+// ---- spread / termination (reduce.hip)
+hipError_t launch_partials_from_x(const double* x, const uint32_t* status, uint64_t B, uint64_t N,
+                                  double2* partial, uint32_t nblk, hipStream_t s);
+hipError_t launch_finalize(const FinalizeArgs& a, uint64_t B, hipStream_t s);
+
+// ---- round kernels
+// Register-resident kernel for RANDOM_REGULAR with a compiled (d, t) pair; returns
+// hipErrorNotSupported (without launching) when (d, t, rule) has no compiled variant.
+bool regular_fast_supported(uint32_t d, uint32_t t, uint32_t rule);
+const char* regular_fast_name(uint32_t d, uint32_t t, bool clean);
+hipError_t launch_round_regular(const RoundArgs& a, uint64_t B, bool clean, hipStream_t s);
+constexpr uint32_t kRegularBlock = 256;
+
+// Generic kernel: one workgroup per receiver, LDS bitonic sort (any topology, m <= 8192).
+constexpr uint32_t kGenericMaxM = 8192;
+hipError_t launch_round_generic(const RoundArgs& a, uint64_t B, hipStream_t s);
+
+// Persistent batched kernel: COMPLETE topology with N <= 64, one wavefront per instance,
+// state in VGPRs across rounds.
+constexpr uint32_t kBatchedMaxN = 64;
+hipError_t launch_batched_small(const BatchArgs& a, uint64_t B, uint32_t k, hipStream_t s);
+const char* batched_small_name(uint32_t N, uint32_t rule);
+
+}  // namespace acs

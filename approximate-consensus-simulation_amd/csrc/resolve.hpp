@@ -1,0 +1,66 @@
+// resolve.hpp — device helpers shared by the round kernels.
+#pragma once
+
+#include "engine.hpp"
+
+namespace acs {
+
+constexpr double kInf = __builtin_huge_val();
+
+// §A.6 resolution of one non-self entry (i <- j, slot s, round r), given the sender's status
+// word, its value x_j, the receiver's x_i and the precomputed §A.5 drop decision.
+__device__ __forceinline__ double resolve_entry(const MsgParams& mp, uint32_t stj, double xj,
+                                                double xi, bool dropped, uint32_t b, uint32_t r,
+                                                uint32_t i, uint64_t s, double lo, double hi) {
+    const bool miss = dropped || crash_missing(mp, stj, b, r, s);
+    if (miss) return xi;
+    if (stj == kByz) return byz_value(mp, b, r, i, s, lo, hi);
+    return xj;
+}
+
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = __builtin_fmin(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = __builtin_fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Block-wide honest (min, max) -> one partial per block (§A.8; min/max are exact and
+// order-free, so any reduction tree gives the oracle's value).
+template <int BS>
+__device__ __forceinline__ void block_minmax_store(double mn, double mx, double2* out) {
+    static_assert(BS % 64 == 0, "block must be whole wavefronts");
+    constexpr int NW = BS / 64;
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    if constexpr (NW == 1) {
+        if (threadIdx.x == 0) *out = make_double2(mn, mx);
+    } else {
+        __shared__ double2 red[NW];
+        const int w = threadIdx.x >> 6;
+        if ((threadIdx.x & 63) == 0) red[w] = make_double2(mn, mx);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double a = red[0].x, c = red[0].y;
+#pragma unroll
+            for (int k = 1; k < NW; ++k) {
+                a = __builtin_fmin(a, red[k].x);
+                c = __builtin_fmax(c, red[k].y);
+            }
+            *out = make_double2(a, c);
+        }
+    }
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+    return __hiloint2double(hi, lo);
+}
+
+}  // namespace acs

@@ -1,0 +1,139 @@
+// round_generic.hip — general-purpose round kernel: one 256-thread workgroup per receiver.
+//
+// Covers every (topology, m <= 8192, rule, t, fault, loss) combination the register kernels do
+// not: the workgroup resolves the m entries (§A.6) into LDS, bitonic-sorts them in LDS padded to
+// a power of two with +inf (§A.7; a sort network, so the sorted sequence — and therefore the
+// tree sum — is the spec's), then applies the rule with an LDS stride-halving tree sum.
+// Used for the dense cfg2 shape (N = 1024 complete, t = 341) and any odd (d, t).
+#include "resolve.hpp"
+
+namespace acs {
+
+constexpr int kGenericBlock = 256;
+
+__device__ __forceinline__ double block_tree_sum(double* w, uint32_t P) {
+    for (uint32_t s = P >> 1; s >= 1; s >>= 1) {
+        for (uint32_t k = threadIdx.x; k < s; k += kGenericBlock) w[k] = w[k] + w[k + s];
+        __syncthreads();
+    }
+    return w[0];
+}
+
+__device__ __forceinline__ void block_bitonic_sort(double* v, uint32_t P) {
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t idx = threadIdx.x; idx < P; idx += kGenericBlock) {
+                const uint32_t ixj = idx ^ j;
+                if (ixj > idx) {
+                    const double p = v[idx], q = v[ixj];
+                    const bool up = (idx & k) == 0;
+                    if (up ? (q < p) : (p < q)) {
+                        v[idx] = q;
+                        v[ixj] = p;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__global__ __launch_bounds__(kGenericBlock) void k_round_generic(const RoundArgs a, uint32_t P) {
+    extern __shared__ __attribute__((aligned(16))) double sh[];  // [P] entries + [P] scratch
+    const uint32_t lb = blockIdx.y, i = blockIdx.x;
+    InstState* S = a.st + lb;
+    if (S->done) return;
+    const uint64_t N = a.N;
+    const double* __restrict__ x = a.xin + lb * N;
+    double* __restrict__ xo = a.xout + lb * N;
+    const uint32_t* stv = a.status ? a.status + lb * N : nullptr;
+    const double xi = x[i];
+    const uint32_t si = stv ? stv[i] : kHonest;
+    const bool honest = si == kHonest;
+    double2* part = a.partial + (uint64_t)lb * a.nblk + i;
+    if (!is_active(si, a.r)) {   // Byzantine or crashed: value frozen (§A.6); never honest
+        if (threadIdx.x == 0) {
+            xo[i] = xi;
+            *part = make_double2(kInf, -kInf);
+        }
+        return;
+    }
+    const MsgParams& mp = a.mp;
+    const uint32_t b = (uint32_t)(mp.inst_offset + lb);
+    const uint32_t bG = b - b % mp.mask_group;
+    const uint32_t r = a.r, m = a.m;
+    const double lo = S->lo, hi = S->hi;
+    const bool avg = a.rule == 0;
+    for (uint32_t e = threadIdx.x; e < P; e += kGenericBlock) {
+        double v;
+        if (e >= m) {
+            v = avg ? 0.0 : kInf;
+        } else {
+            uint32_t j;
+            uint64_t slot;
+            bool self;
+            if (a.topology == 0) {   // COMPLETE: entry j from node j, slot i*N + j
+                j = e;
+                slot = (uint64_t)i * N + j;
+                self = j == i;
+            } else {                 // RANDOM_REGULAR: entry 0 self, entry 1+t from nbr(i,t)
+                self = e == 0;
+                const uint32_t t = e - 1;
+                j = self ? i : a.ell[(((uint64_t)(i >> 6) * (a.dp >> 2) + (t >> 2)) * 64 + (i & 63)) * 4 + (t & 3)];
+                slot = (uint64_t)i * a.d + t;
+            }
+            if (self) {
+                v = xi;
+            } else {
+                const uint32_t stj = stv ? stv[j] : kHonest;
+                const bool dropped = mp.thr && draw(mp.key, kStreamDrop, bG, r, slot) < mp.thr;
+                v = resolve_entry(mp, stj, x[j], xi, dropped, b, r, i, slot, lo, hi);
+            }
+        }
+        sh[e] = v;
+    }
+    __syncthreads();
+    double res;
+    if (avg) {
+        res = block_tree_sum(sh, P) / (double)m;
+    } else {
+        block_bitonic_sort(sh, P);
+        const uint32_t t = a.trim, nr = m - 2 * t;
+        if (a.rule == 2) {
+            res = (sh[t] + sh[m - t - 1]) * 0.5;
+        } else {
+            const uint32_t step = a.rule == 3 ? t : 1;
+            const uint32_t cnt = a.rule == 3 ? (nr + t - 1) / t : nr;
+            uint32_t P2 = 1;
+            while (P2 < cnt) P2 <<= 1;
+            double* w = sh + P;
+            for (uint32_t k = threadIdx.x; k < P2; k += kGenericBlock) w[k] = k < cnt ? sh[t + k * step] : 0.0;
+            __syncthreads();
+            res = block_tree_sum(w, P2) / (double)cnt;
+        }
+    }
+    if (threadIdx.x == 0) {
+        xo[i] = res;
+        *part = honest ? make_double2(res, res) : make_double2(kInf, -kInf);
+    }
+}
+
+hipError_t launch_round_generic(const RoundArgs& a, uint64_t B, hipStream_t s) {
+    uint32_t P = 1;
+    while (P < a.m) P <<= 1;
+    if (P > kGenericMaxM) return hipErrorNotSupported;
+    const size_t lds = 2 * (size_t)P * sizeof(double);
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_round_generic,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)(2 * kGenericMaxM * sizeof(double)));
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    const dim3 grid((unsigned)a.N, (unsigned)B);
+    hipLaunchKernelGGL(k_round_generic, grid, dim3(kGenericBlock), lds, s, a, P);
+    return hipGetLastError();
+}
+
+}  // namespace acs

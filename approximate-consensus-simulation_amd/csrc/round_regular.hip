@@ -1,0 +1,163 @@
+// round_regular.hip — the headline hot-path kernel (SURVEY §8(a) a5+a7+a8+a9, cfg4/cfg5).
+//
+// One lane = one receiver i of a RANDOM_REGULAR graph with a compile-time degree D and trim T.
+// Per lane and round:
+//   - D/4 coalesced 16-byte loads of neighbour ids (the wave reads 1 KiB contiguous per group);
+//   - D random 8-byte gathers of x_j (issued together: D loads in flight per lane);
+//   - [faults/loss only] status gathers, one Philox call per 4 slots for the drop mask (§A.5),
+//     crash / Byzantine resolution (§A.4, §A.6);
+//   - a compile-time selection network over the m = D+1 entries kept in VGPRs (§A.7; only the
+//     comparators that reach the window [T, m-T) survive pruning);
+//   - the rule (tree sum in the §A.7 order + IEEE divide, or the midpoint), one 8-byte store;
+//   - honest (min, max) of x^{r+1} reduced per block -> one partial (§A.8 epilogue).
+// Algorithmic traffic (no faults, no loss): 4D + 8D + 8 + 8 bytes per node-round (400 B at
+// D = 32).  Everything is bit-exact with the spec: no FMA (-ffp-contract=off), IEEE division.
+#include "resolve.hpp"
+#include "sortnet.hpp"
+
+namespace acs {
+
+template <int D, int T>
+__device__ __forceinline__ double apply_rule_reg(uint32_t rule, double (&v)[D + 1]) {
+    constexpr int M = D + 1;
+    if constexpr (T == 0) {
+        if (rule == 0) return tree_sum_const<M>(v) / (double)M;   // AVERAGE: entry order
+    }
+    select_sort<M, T, M - T>(v);
+    constexpr int NR = M - 2 * T;
+    if (rule == 2) return (v[T] + v[M - T - 1]) * 0.5;                // MIDPOINT
+    if constexpr (T >= 1) {
+        if (rule == 3) {                                             // DLPSW: R[0], R[T], ...
+            constexpr int NQ = (NR + T - 1) / T;
+            return tree_sum_const<NQ, T, T>(v) / (double)NQ;
+        }
+    }
+    return tree_sum_const<NR, T>(v) / (double)NR;                    // TRIMMED_MEAN
+}
+
+template <int D, int T, bool CLEAN>
+__global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs a) {
+    static_assert(D % 4 == 0, "compiled degrees are multiples of 4");
+    constexpr int M = D + 1;
+    constexpr int NQ = D / 4;
+    const uint32_t lb = blockIdx.y;
+    InstState* S = a.st + lb;
+    if (S->done) return;  // device-side early exit (uniform per block)
+
+    const uint64_t N = a.N;
+    const double* __restrict__ x = a.xin + lb * N;
+    double* __restrict__ xo = a.xout + lb * N;
+    const uint32_t i = blockIdx.x * kRegularBlock + threadIdx.x;
+
+    double mn = kInf, mx = -kInf;
+    if (i < N) {
+        const double xi = x[i];
+        double res = xi;
+        bool honest = true, active = true;
+        const uint32_t* stv = nullptr;
+        if constexpr (!CLEAN) {
+            stv = a.status + lb * N;
+            const uint32_t si = stv[i];
+            honest = si == kHonest;
+            active = is_active(si, a.r);
+        }
+        if (active) {
+            const uint4* cp = reinterpret_cast<const uint4*>(a.ell) +
+                              (uint64_t)(i >> 6) * (NQ * 64) + (i & 63);
+            uint32_t col[D];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const uint4 c = cp[q * 64];
+                col[4 * q + 0] = c.x;
+                col[4 * q + 1] = c.y;
+                col[4 * q + 2] = c.z;
+                col[4 * q + 3] = c.w;
+            }
+            double v[M];
+            v[0] = xi;
+            if constexpr (CLEAN) {
+#pragma unroll
+                for (int t = 0; t < D; ++t) v[1 + t] = x[col[t]];
+            } else {
+                const MsgParams& mp = a.mp;
+                const uint32_t b = (uint32_t)(mp.inst_offset + lb);
+                const uint32_t bG = b - b % mp.mask_group;
+                const double lo = S->lo, hi = S->hi;
+                const uint32_t r = a.r;
+                double xj[D];
+                uint32_t sj[D];
+#pragma unroll
+                for (int t = 0; t < D; ++t) {   // all gathers first, unconditionally
+                    xj[t] = x[col[t]];
+                    sj[t] = stv[col[t]];
+                }
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    // slots s = i*D + 4q .. +3 share Philox counter s>>2 = i*(D/4) + q (§A.5)
+                    U4 w;
+                    w.v[0] = w.v[1] = w.v[2] = w.v[3] = 0xFFFFFFFFu;
+                    if (mp.thr) w = philox10(i * (uint32_t)NQ + q, r, bG, kStreamDrop, mp.key);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int t = 4 * q + e;
+                        const uint64_t s = (uint64_t)i * D + t;
+                        const bool dropped = w.v[e] < mp.thr;
+                        v[1 + t] = resolve_entry(mp, sj[t], xj[t], xi, dropped, b, r, i, s, lo, hi);
+                    }
+                }
+            }
+            res = apply_rule_reg<D, T>(a.rule, v);
+        }
+        xo[i] = res;
+        if (honest) {
+            mn = res;
+            mx = res;
+        }
+    }
+    block_minmax_store<kRegularBlock>(mn, mx, a.partial + (uint64_t)lb * a.nblk + blockIdx.x);
+}
+
+// ---------------------------------------------------------------------------- dispatch
+// (D, T) pairs compiled into the register path; anything else uses the generic kernel.
+#define ACS_REGULAR_VARIANTS(X) \
+    X(4, 0) X(4, 1) X(8, 0) X(8, 2) X(16, 0) X(16, 5) X(32, 0) X(32, 5)
+
+static bool rule_ok(uint32_t t, uint32_t rule) {
+    if (rule == 0) return t == 0;     // AVERAGE
+    if (rule == 3) return t >= 1;     // DLPSW
+    return rule == 1 || rule == 2;
+}
+
+bool regular_fast_supported(uint32_t d, uint32_t t, uint32_t rule) {
+#define X(DD, TT) if (d == DD && t == TT) return rule_ok(t, rule);
+    ACS_REGULAR_VARIANTS(X)
+#undef X
+    return false;
+}
+
+const char* regular_fast_name(uint32_t d, uint32_t t, bool clean) {
+#define X(DD, TT)                                                                          \
+    if (d == DD && t == TT)                                                                \
+        return clean ? "k_round_regular<" #DD "," #TT ",clean>" : "k_round_regular<" #DD "," #TT ",faulty>";
+    ACS_REGULAR_VARIANTS(X)
+#undef X
+    return "k_round_regular<?>";
+}
+
+hipError_t launch_round_regular(const RoundArgs& a, uint64_t B, bool clean, hipStream_t s) {
+    const dim3 grid((unsigned)((a.N + kRegularBlock - 1) / kRegularBlock), (unsigned)B);
+    const dim3 block(kRegularBlock);
+#define X(DD, TT)                                                                         \
+    if (a.d == DD && a.trim == TT) {                                                      \
+        if (clean)                                                                        \
+            hipLaunchKernelGGL((k_round_regular<DD, TT, true>), grid, block, 0, s, a);    \
+        else                                                                              \
+            hipLaunchKernelGGL((k_round_regular<DD, TT, false>), grid, block, 0, s, a);   \
+        return hipGetLastError();                                                         \
+    }
+    ACS_REGULAR_VARIANTS(X)
+#undef X
+    return hipErrorNotSupported;
+}
+
+}  // namespace acs

@@ -1,0 +1,117 @@
+// setup.hip — one-time device setup: initial values, the Feistel
+// graph as an ELL slice layout, and the fault schedule.  Not timed as the hot path, but
+// bit-exact with the spec like everything else.
+#include <hipcub/hipcub.hpp>
+
+#include "engine.hpp"
+
+namespace acs {
+
+// §A.2: x_i^0 = u53(draw(INIT,b,0,2i), draw(INIT,b,0,2i+1)); both words come from one Philox
+// call (counter (2i)>>2 = i>>1, words 2(i&1) and 2(i&1)+1).
+__global__ __launch_bounds__(256) void k_init_values(double* x, uint64_t N, Key key, uint64_t inst_offset) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t lb = blockIdx.y;
+    if (i >= N) return;
+    const uint32_t b = (uint32_t)(inst_offset + lb);
+    const U4 w = philox10((uint32_t)(i >> 1), 0u, b, kStreamInit, key);
+    const uint32_t sel = (uint32_t)((i & 1u) << 1);
+    x[lb * N + i] = u53(pick(w, sel), pick(w, sel + 1));
+}
+
+// §A.3: column t of node i is π_{t/2}(i) (t even) or π_{t/2}^{-1}(i) (t odd).
+__global__ __launch_bounds__(256) void k_build_ell(uint32_t* ell, uint64_t N, uint32_t d, uint32_t dp,
+                                                   Feistel f) {
+    const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t half = d >> 1;
+    const uint64_t i = gid / half;
+    const uint32_t k = (uint32_t)(gid % half);
+    if (i >= N) return;
+    const uint32_t fw = feistel_fwd(f, k, (uint32_t)i);
+    const uint32_t iv = feistel_inv(f, k, (uint32_t)i);
+    const uint64_t base = ((i >> 6) * (dp >> 2)) * 256 + (i & 63) * 4;
+    const uint32_t t0 = 2 * k, t1 = 2 * k + 1;
+    ell[base + (uint64_t)(t0 >> 2) * 256 + (t0 & 3)] = fw;
+    ell[base + (uint64_t)(t1 >> 2) * 256 + (t1 & 3)] = iv;
+}
+
+__global__ __launch_bounds__(256) void k_fault_keys(uint64_t* keys, uint64_t N, Key key, uint64_t inst_offset) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t lb = blockIdx.y;
+    if (i >= N) return;
+    const uint32_t b = (uint32_t)(inst_offset + lb);
+    keys[lb * N + i] = ((uint64_t)draw(key, kStreamFaultset, b, 0, i) << 32) | i;
+}
+
+__global__ __launch_bounds__(256) void k_fill_u32(uint32_t* p, uint64_t n, uint32_t v) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) p[i] = v;
+}
+
+// §A.4: the f smallest (key, i) pairs of each instance are faulty.
+__global__ __launch_bounds__(256) void k_mark_faults(uint32_t* status, const uint64_t* sorted, uint64_t N,
+                                                     uint32_t f, uint32_t model, uint32_t W, Key key,
+                                                     uint64_t inst_offset) {
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t lb = blockIdx.y;
+    if (k >= f) return;
+    const uint32_t b = (uint32_t)(inst_offset + lb);
+    const uint32_t v = (uint32_t)(sorted[lb * N + k] & 0xFFFFFFFFu);
+    status[lb * N + v] = model == 2 ? kByz : draw(key, kStreamCrashRound, b, 0, v) % W;
+}
+
+struct SegOffset {
+    uint64_t N;
+    __host__ __device__ uint64_t operator()(uint64_t b) const { return b * N; }
+};
+
+hipError_t launch_init_values(double* x, uint64_t B, uint64_t N, Key key, uint64_t inst_offset,
+                              hipStream_t s) {
+    hipLaunchKernelGGL(k_init_values, dim3((unsigned)((N + 255) / 256), (unsigned)B), dim3(256), 0, s, x, N,
+                       key, inst_offset);
+    return hipGetLastError();
+}
+
+hipError_t launch_build_ell(uint32_t* ell, uint64_t N, uint32_t d, uint32_t dp, const Feistel& f,
+                            hipStream_t s) {
+    const uint64_t work = N * (d >> 1);
+    hipLaunchKernelGGL(k_build_ell, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, ell, N, d, dp, f);
+    return hipGetLastError();
+}
+
+hipError_t build_fault_status(uint32_t* status, uint64_t B, uint64_t N, uint32_t f,
+                              uint32_t fault_model, uint32_t crash_window, Key key,
+                              uint64_t inst_offset, hipStream_t s) {
+    hipError_t e;
+    const uint64_t n = B * N;
+    hipLaunchKernelGGL(k_fill_u32, dim3(1024), dim3(256), 0, s, status, n, kHonest);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (fault_model == 0 || f == 0) return hipSuccess;
+    uint64_t *keys = nullptr, *sorted = nullptr;
+    void* temp = nullptr;
+    size_t temp_bytes = 0;
+    if ((e = hipMalloc(&keys, n * sizeof(uint64_t))) != hipSuccess) return e;
+    if ((e = hipMalloc(&sorted, n * sizeof(uint64_t))) != hipSuccess) { (void)hipFree(keys); return e; }
+    hipLaunchKernelGGL(k_fault_keys, dim3((unsigned)((N + 255) / 256), (unsigned)B), dim3(256), 0, s, keys, N,
+                       key, inst_offset);
+    auto offs = hipcub::TransformInputIterator<uint64_t, SegOffset, hipcub::CountingInputIterator<uint64_t>>(
+        hipcub::CountingInputIterator<uint64_t>(0), SegOffset{N});
+    e = hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, temp_bytes, keys, sorted, (int)n, (int)B, offs,
+                                                   offs + 1, 0, 64, s);
+    if (e == hipSuccess) e = hipMalloc(&temp, temp_bytes ? temp_bytes : 16);
+    if (e == hipSuccess)
+        e = hipcub::DeviceSegmentedRadixSort::SortKeys(temp, temp_bytes, keys, sorted, (int)n, (int)B, offs,
+                                                       offs + 1, 0, 64, s);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_mark_faults, dim3((f + 255) / 256, (unsigned)B), dim3(256), 0, s, status, sorted,
+                           N, f, fault_model, crash_window, key, inst_offset);
+        e = hipGetLastError();
+    }
+    hipError_t e2 = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = e2;
+    (void)hipFree(temp);
+    (void)hipFree(sorted);
+    (void)hipFree(keys);
+    return e;
+}
+
+}  // namespace acs

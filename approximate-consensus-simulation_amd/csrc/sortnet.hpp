@@ -1,0 +1,118 @@
+// sortnet.hpp — compile-time sorting / selection networks kept entirely in VGPRs.
+//
+// Batcher's odd–even merge sort on P = 2^k wires, pruned in two ways at compile time:
+//  1. to M <= P live inputs (comparators touching wires >= M are dropped; the network still
+//     sorts the first M wires because padding wires would hold +inf and never move);
+//  2. to an output window [LO, HI): comparators whose outputs never reach a window position
+//     are dropped (backward liveness).  SURVEY §8(a) a7: the trimmed mean needs only the sorted
+//     middle R = S[t .. m-t), e.g. 239 instead of 246 comparators for m = 33, t = 5.
+// Every comparator index is a template constant, so the value array never leaves registers.
+#pragma once
+
+#include <stdint.h>
+
+#include <utility>
+
+namespace acs {
+
+struct CE {
+    int16_t a, b;
+};
+
+template <int CAP>
+struct CEList {
+    CE c[CAP];
+    int n;
+};
+
+constexpr int ce_cap(int P) { return P * P / 2 + 8; }
+
+template <int P>
+constexpr CEList<ce_cap(P)> batcher_all() {
+    CEList<ce_cap(P)> L{};
+    L.n = 0;
+    for (int p = 1; p < P; p <<= 1)
+        for (int k = p; k >= 1; k >>= 1)
+            for (int j = k % p; j + k < P; j += 2 * k)
+                for (int i = 0; i < (k < P - j - k ? k : P - j - k); ++i)
+                    if ((i + j) / (2 * p) == (i + j + k) / (2 * p)) {
+                        L.c[L.n].a = (int16_t)(i + j);
+                        L.c[L.n].b = (int16_t)(i + j + k);
+                        ++L.n;
+                    }
+    return L;
+}
+
+template <int P, int M, int LO, int HI>
+constexpr CEList<ce_cap(P)> pruned_net() {
+    const auto all = batcher_all<P>();
+    CEList<ce_cap(P)> tmp{};
+    tmp.n = 0;
+    for (int q = 0; q < all.n; ++q)
+        if (all.c[q].b < M) tmp.c[tmp.n++] = all.c[q];
+    bool need[P] = {};
+    for (int w = 0; w < P; ++w) need[w] = (w >= LO && w < HI);
+    bool keep[ce_cap(P)] = {};
+    for (int q = tmp.n - 1; q >= 0; --q) {
+        const int a = tmp.c[q].a, b = tmp.c[q].b;
+        if (need[a] || need[b]) {
+            keep[q] = true;
+            need[a] = need[b] = true;
+        }
+    }
+    CEList<ce_cap(P)> out{};
+    out.n = 0;
+    for (int q = 0; q < tmp.n; ++q)
+        if (keep[q]) out.c[out.n++] = tmp.c[q];
+    return out;
+}
+
+constexpr int next_pow2(int n) {
+    int p = 1;
+    while (p < n) p <<= 1;
+    return p;
+}
+
+template <int M, int LO, int HI>
+struct SelectNet {
+    static constexpr int P = next_pow2(M);
+    static constexpr auto list = pruned_net<P, M, LO, HI>();
+    static constexpr int count = list.n;
+};
+
+template <int A, int B, typename T, int M>
+__device__ __forceinline__ void cmpx(T (&v)[M]) {
+    const T a = v[A], b = v[B];
+    v[A] = __builtin_fmin(a, b);
+    v[B] = __builtin_fmax(a, b);
+}
+
+template <typename Net, typename T, int M, size_t... I>
+__device__ __forceinline__ void run_net(T (&v)[M], std::index_sequence<I...>) {
+    (cmpx<Net::list.c[I].a, Net::list.c[I].b>(v), ...);
+}
+
+// Sort v[0..M) so that positions [LO, HI) hold the ascending order statistics LO..HI-1.
+template <int M, int LO = 0, int HI = M, typename T>
+__device__ __forceinline__ void select_sort(T (&v)[M]) {
+    using Net = SelectNet<M, LO, HI>;
+    run_net<Net>(v, std::make_index_sequence<Net::count>{});
+}
+
+// §A.7 tree_sum over N values a[OFF], a[OFF+STRIDE], ...: pad to a power of two with +0.0,
+// stride-halving pairwise adds.  Compile-time indices only.
+template <int N, int OFF = 0, int STRIDE = 1, typename T, int M>
+__device__ __forceinline__ T tree_sum_const(const T (&a)[M]) {
+    constexpr int P = next_pow2(N);
+    T w[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) w[k] = k < N ? a[OFF + k * STRIDE] : T(0);
+#pragma unroll
+    for (int s = P / 2; s >= 1; s >>= 1) {
+#pragma unroll
+        for (int k = 0; k < s; ++k) w[k] = w[k] + w[k + s];
+    }
+    return w[0];
+}
+
+}  // namespace acs

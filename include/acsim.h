@@ -1,0 +1,185 @@
+/*
+ * acsim.h — C ABI of the MI355X-native approximate-consensus round engine.
+ *
+ * Provenance.  The upstream reference (Dariusrussellkish/approximate-consensus-simulation,
+ * mounted at /root/reference) holds exactly one file, README.md:1 ("# eventual-consensus-simulation"),
+ * and no code.  There is therefore no upstream function this ABI can replace line for line; every
+ * entry point below replaces the spec-level operation named in SURVEY.md §8(a)/(b), and the
+ * semantics are those of SURVEY.md Appendix A (the frozen spec that stands in for the missing
+ * reference).  Each declaration cites the §8 row / §A section it implements.
+ *
+ * Conventions.
+ *  - Plain C, no C++ or torch types: pointers, sizes and POD structs only.
+ *  - Every function returns 0 (ACS_OK) or a negative ACS_E* status; no exceptions cross the ABI.
+ *    acs_last_error() returns a thread-local message for the last non-zero status.
+ *  - The handle owns every device buffer.  Callers own the host buffers they pass in; the library
+ *    copies into / out of them and retains no pointer after return.
+ *  - A handle is not thread-safe; distinct handles may be used from distinct threads.
+ */
+#ifndef ACSIM_H
+#define ACSIM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ACS_ABI_VERSION 1
+
+/* status codes */
+#define ACS_OK            0
+#define ACS_EINVAL       (-1)
+#define ACS_ENOMEM       (-2)
+#define ACS_EDEVICE      (-3)
+#define ACS_ECOMM        (-4)
+#define ACS_EUNSUPPORTED (-5)
+
+/* backends.  The product library implements ACS_HIP only; the CPU spec reference lives in
+ * oracle/ as test infrastructure and is not reachable through this library (ACS_CPU returns
+ * ACS_EUNSUPPORTED here). */
+#define ACS_CPU 0
+#define ACS_HIP 1
+
+/* topology (§A.3) */
+#define ACS_TOPO_COMPLETE        0
+#define ACS_TOPO_RANDOM_REGULAR  1
+
+/* update rule (§A.7) */
+#define ACS_RULE_AVERAGE       0
+#define ACS_RULE_TRIMMED_MEAN  1
+#define ACS_RULE_MIDPOINT      2
+#define ACS_RULE_DLPSW_SELECT  3
+
+/* fault model (§A.4) */
+#define ACS_FAULT_NONE       0
+#define ACS_FAULT_CRASH      1
+#define ACS_FAULT_BYZANTINE  2
+
+/* Byzantine strategy (§A.4) */
+#define ACS_BYZ_SPLIT     0
+#define ACS_BYZ_RANDOM    1
+#define ACS_BYZ_CONSTANT  2
+
+/* termination (§A.8) */
+#define ACS_TERM_EPS    0
+#define ACS_TERM_FIXED  1
+
+/* value type (§A.0).  Only ACS_F64 is implemented in this round. */
+#define ACS_F64 0
+#define ACS_F32 1
+
+/* Philox streams (§A.1) */
+#define ACS_STREAM_INIT          0u
+#define ACS_STREAM_DROP          1u
+#define ACS_STREAM_FAULTSET      2u
+#define ACS_STREAM_CRASH_ROUND   3u
+#define ACS_STREAM_CRASH_PARTIAL 4u
+#define ACS_STREAM_BYZ           5u
+#define ACS_STREAM_GRAPH         6u
+
+/* Opaque simulation handle. */
+typedef struct acs_sim acs_sim;
+
+/* One simulation configuration.  POD; struct_size must equal sizeof(acs_config). */
+typedef struct acs_config {
+    uint32_t struct_size;
+    uint64_t n_nodes;          /* N */
+    uint64_t n_instances;      /* B: independent instances held by this handle */
+    uint32_t topology;         /* ACS_TOPO_* */
+    uint32_t degree;           /* d (even, >= 2) for RANDOM_REGULAR */
+    uint32_t rule;             /* ACS_RULE_* */
+    uint32_t trim;             /* t */
+    uint32_t fault_model;      /* ACS_FAULT_* */
+    uint32_t n_faulty;         /* f */
+    uint32_t byz_strategy;     /* ACS_BYZ_* */
+    double   byz_delta;        /* Δ */
+    double   byz_const;        /* c */
+    uint32_t crash_window;     /* W >= 1 */
+    double   loss_p;           /* message-loss probability in [0,1) */
+    uint32_t mask_group;       /* G >= 1: instances b with equal b - b%G share drop masks */
+    double   eps;              /* ε */
+    uint32_t max_rounds;       /* round cap (EPS) or exact round count (FIXED) */
+    uint32_t termination;      /* ACS_TERM_* */
+    uint32_t dtype;            /* ACS_F64 */
+    uint64_t seed;             /* Philox key for every stream except GRAPH */
+    uint64_t graph_seed;       /* Philox key for GRAPH; 0 means "use seed" */
+    uint32_t trace_spread;     /* 1: keep spread^r for every round (per instance) */
+    uint32_t omp_threads;      /* CPU oracle only; ignored by the HIP library */
+    uint64_t instance_offset;  /* global id of local instance 0 (multi-GPU instance sharding, §8e) */
+} acs_config;
+
+/* Result of acs_round. For B > 1: round = max rounds over instances,
+ * spread = max current spread over instances, lo/hi = instance 0's honest min/max. */
+typedef struct acs_round_info {
+    uint32_t round;            /* rounds executed so far (max over instances) */
+    uint32_t done;             /* 1 when every instance has terminated */
+    double   spread;
+    double   lo;
+    double   hi;
+    uint64_t instances_done;
+} acs_round_info;
+
+/* Result of acs_run. */
+typedef struct acs_result {
+    uint32_t rounds_max;       /* max over instances of rounds executed */
+    uint32_t n_converged;      /* instances with final spread <= eps */
+    uint64_t node_rounds;      /* Σ_b N · rounds_executed(b) */
+    double   wall_seconds;     /* host wall time of this call */
+    double   final_spread_max; /* max over instances of final spread */
+    uint64_t n_instances;
+} acs_result;
+
+/* §8b: create a simulation (validates the §A.8 constraints, allocates HBM, builds the graph,
+ * the fault schedule and x^0 on the device).  devices/n_devices: exactly one device id. */
+int acs_create(const acs_config* cfg, int backend, const int* devices, int n_devices,
+               struct acs_sim** out);
+
+/* §8(a) a10/a9: advance every unfinished instance by at most k rounds; stops at convergence. */
+int acs_round(struct acs_sim* sim, uint32_t k, acs_round_info* out);
+
+/* §8(a) a11: run to convergence (EPS) or exactly max_rounds (FIXED). */
+int acs_run(struct acs_sim* sim, acs_result* out);
+
+/* Copy instance's current node values (N values of the config dtype) into a caller buffer. */
+int acs_get_values(struct acs_sim* sim, uint64_t instance, void* out, uint64_t n);
+
+/* Per-instance rounds executed / converged flag / current spread. */
+int acs_get_instance_rounds(struct acs_sim* sim, uint32_t* out, uint64_t n_instances);
+int acs_get_instance_converged(struct acs_sim* sim, uint8_t* out, uint64_t n_instances);
+int acs_get_instance_spread(struct acs_sim* sim, double* out, uint64_t n_instances);
+
+/* Spread trace spread^0..spread^rounds of one instance (needs trace_spread = 1).
+ * *n_out receives the number of values written (rounds + 1, capped at n). */
+int acs_get_spread_trace(struct acs_sim* sim, uint64_t instance, double* out, uint64_t n,
+                         uint64_t* n_out);
+
+/* Resume (§A.9): set every instance to round `round` with values x (B*N values, instance-major).
+ * Instances become unfinished unless the EPS test already holds at `round`. */
+int acs_set_state(struct acs_sim* sim, uint32_t round, const void* x, uint64_t n);
+
+/* Device-side fault schedule (§A.4): per node u32 status, 0xFFFFFFFF honest, 0xFFFFFFFE
+ * Byzantine, otherwise the crash round r_v.  out holds B*N words. */
+int acs_get_fault_status(struct acs_sim* sim, uint32_t* out, uint64_t n);
+
+/* Adjacency (§A.3) of a RANDOM_REGULAR graph: out[i*d + t] = nbr(i, t). */
+int acs_get_neighbors(struct acs_sim* sim, uint32_t* out, uint64_t n);
+
+/* Kernel timing (bench measurement, §8d): while enabled, HIP events bracket every launch of
+ * the round kernel on the handle's stream; acs_get_kernel_timing returns the summed device time
+ * and launch count since the last reset, plus the name of the round kernel in use. */
+int acs_set_kernel_timing(struct acs_sim* sim, int enable);
+int acs_get_kernel_timing(struct acs_sim* sim, double* total_ms, uint64_t* launches,
+                          char* kernel_name, uint64_t name_cap);
+
+/* Wait for all device work of this handle. */
+int acs_sync(struct acs_sim* sim);
+
+void acs_destroy(struct acs_sim* sim);
+const char* acs_last_error(void);
+int acs_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ACSIM_H */

@@ -1,0 +1,202 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the CPU oracle on the same seeds.
+
+Bar (BASELINE.json north_star): identical rounds-to-convergence, bit-exact drop masks / fault
+schedules, final values — here every path is VALU fp64 without FMA, so the bar applied is
+bit-exact equality of the final values and of the spread trace (stricter than 1e-12 relative).
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import acsim
+from acsim.config import Config, preset
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
+
+
+def bits(a):
+    return np.ascontiguousarray(a, dtype=np.float64).view(np.uint64)
+
+
+def run_both(oracle_mod, cfg, threads=8):
+    with acsim.Simulator(cfg, device=0) as g:
+        g.run()
+        gres = dict(rounds=g.rounds(), conv=g.converged(), x=g.all_values(), spread=g.spread(),
+                    status=g.fault_status(),
+                    trace=[g.spread_trace(b) for b in range(min(cfg.n_instances, 4))] if cfg.trace_spread else None)
+    with oracle_mod.OracleSimulator(cfg, threads=threads) as o:
+        o.run()
+        ores = dict(rounds=o.rounds(), conv=o.converged(), x=o.all_values(), spread=o.spread(),
+                    status=o.fault_status(),
+                    trace=[o.spread_trace(b) for b in range(min(cfg.n_instances, 4))] if cfg.trace_spread else None)
+    return gres, ores
+
+
+def assert_same(g, o):
+    assert np.array_equal(g["rounds"], o["rounds"]), (g["rounds"][:8], o["rounds"][:8])
+    assert np.array_equal(g["conv"], o["conv"])
+    assert np.array_equal(g["status"], o["status"]), "fault schedules differ"
+    assert np.array_equal(bits(g["x"]), bits(o["x"])), "final values differ"
+    assert np.array_equal(bits(g["spread"]), bits(o["spread"]))
+    if g["trace"] is not None:
+        for a, b in zip(g["trace"], o["trace"]):
+            assert np.array_equal(bits(a), bits(b)), "spread traces differ"
+
+
+@pytest.mark.parametrize("name", sorted(GOLDEN["sims"]))
+def test_gpu_matches_golden_and_oracle(oracle_mod, name):
+    g = GOLDEN["sims"][name]
+    cfg = Config(**g["config"])
+    with acsim.Simulator(cfg, device=0) as s:
+        s.run()
+        assert s.rounds().tolist() == g["rounds"]
+        assert s.converged().tolist() == g["converged"]
+        for b in range(cfg.n_instances):
+            x = s.values(b)
+            assert hashlib.sha256(x.tobytes()).hexdigest() == g["x_sha256"][b], f"instance {b}"
+        for b, tr in enumerate(g["trace"]):
+            assert [float(v).hex() for v in s.spread_trace(b)] == tr
+        st = s.fault_status()
+        for b, fl in enumerate(g["faulty"]):
+            assert np.nonzero(st[b] != 0xFFFFFFFF)[0].tolist() == fl
+
+
+CASES = {
+    # headline kernel, clean, full size EPS (≈ 14 rounds) — every value bit-exact
+    "cfg4_full_eps": preset("cfg4_eps", trace_spread=True),
+    "cfg4_full_fixed20": preset("cfg4", max_rounds=20, trace_spread=True),
+    "cfg4_byz_full": preset("cfg4_byz", trace_spread=True),
+    "cfg4_drop_crash": preset("cfg4_eps", n_nodes=100000, loss_p=0.2, fault_model="crash",
+                              n_faulty=1000, crash_window=4, trace_spread=True),
+    "cfg5_shape_n2e18": preset("cfg5", n_nodes=1 << 18, max_rounds=12, trace_spread=True),
+    "reg16_t5_byzsplit_drop": Config(n_nodes=50000, topology="regular", degree=16, rule="trimmed",
+                                     trim=5, fault_model="byzantine", n_faulty=2000,
+                                     byz_strategy="split", byz_delta=0.2, loss_p=0.1, eps=1e-7,
+                                     max_rounds=400, seed=17, trace_spread=True),
+    "reg8_mid_byzconst": Config(n_nodes=30001, topology="regular", degree=8, rule="midpoint", trim=2,
+                                fault_model="byzantine", n_faulty=300, byz_strategy="constant",
+                                byz_const=-3.0, eps=1e-7, max_rounds=400, seed=4, trace_spread=True),
+    "reg32_avg": Config(n_nodes=20000, topology="regular", degree=32, rule="average", eps=1e-9,
+                        max_rounds=200, seed=8, trace_spread=True),
+    "reg32_dlpsw": Config(n_nodes=20000, topology="regular", degree=32, rule="dlpsw", trim=5,
+                          loss_p=0.05, eps=1e-9, max_rounds=200, seed=8, trace_spread=True),
+    "reg4_t1_multi_instance": Config(n_nodes=5000, n_instances=5, topology="regular", degree=4,
+                                     rule="trimmed", trim=1, loss_p=0.1, mask_group=2, eps=1e-6,
+                                     max_rounds=3000, seed=12, instance_offset=9, trace_spread=True),
+    # generic kernel (odd d / t, dense complete graphs)
+    "generic_reg10_t3": Config(n_nodes=7000, topology="regular", degree=10, rule="trimmed", trim=3,
+                               fault_model="crash", n_faulty=100, crash_window=6, loss_p=0.05,
+                               eps=1e-8, max_rounds=500, seed=1, trace_spread=True),
+    "generic_complete200_byzrand": Config(n_nodes=200, topology="complete", rule="trimmed", trim=20,
+                                          fault_model="byzantine", n_faulty=20,
+                                          byz_strategy="random", byz_delta=0.3, loss_p=0.1,
+                                          eps=1e-8, max_rounds=500, seed=6, trace_spread=True),
+    "generic_complete65_avg": Config(n_nodes=65, n_instances=3, topology="complete", rule="average",
+                                     loss_p=0.2, eps=1e-9, max_rounds=300, seed=2, trace_spread=True),
+    "cfg2_full": preset("cfg2", trace_spread=True),
+    # batched persistent kernel (complete, N <= 64)
+    "cfg1": preset("cfg1", trace_spread=True),
+    "cfg1_avg": preset("cfg1_avg", trace_spread=True),
+    "cfg3_b4096": preset("cfg3", n_instances=4096, trace_spread=True),
+    "batched13_crash_mid": Config(n_nodes=13, n_instances=50, topology="complete", rule="midpoint",
+                                  trim=2, fault_model="crash", n_faulty=3, crash_window=3,
+                                  loss_p=0.3, eps=1e-9, max_rounds=300, seed=5, trace_spread=True),
+    "batched64_trim_byz": Config(n_nodes=64, n_instances=40, topology="complete", rule="trimmed",
+                                 trim=10, fault_model="byzantine", n_faulty=10,
+                                 byz_strategy="random", byz_delta=0.05, loss_p=0.1, eps=1e-9,
+                                 max_rounds=300, seed=14, trace_spread=True),
+    "batched32_dlpsw_fixed": Config(n_nodes=32, n_instances=33, topology="complete", rule="dlpsw",
+                                    trim=4, eps=0.0, max_rounds=40, termination="fixed",
+                                    loss_p=0.3, mask_group=8, seed=3, trace_spread=True),
+}
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_gpu_matches_oracle(oracle_mod, name):
+    g, o = run_both(oracle_mod, CASES[name])
+    assert_same(g, o)
+
+
+def test_cfg3_full_batch_sampled(oracle_mod):
+    """1e5 instances on the GPU; a sample of instance windows re-run on the oracle through
+    instance_offset (instances are independent and seeded by their global id)."""
+    cfg = preset("cfg3")
+    with acsim.Simulator(cfg, device=0) as g:
+        res = g.run()
+        rounds = g.rounds()
+        assert res.n_converged == cfg.n_instances
+        samples = {b0: [g.values(b) for b in range(b0, b0 + 8)] for b0 in (0, 31337, 99992)}
+    for b0, xs in samples.items():
+        sub = cfg.replace(n_instances=8, instance_offset=b0)
+        with oracle_mod.OracleSimulator(sub) as o:
+            o.run()
+            assert np.array_equal(o.rounds(), rounds[b0:b0 + 8])
+            for k in range(8):
+                assert np.array_equal(bits(o.values(k)), bits(xs[k]))
+
+
+def test_neighbors_and_status_match(oracle_mod):
+    cfg = preset("cfg4_byz", n_nodes=10007, n_faulty=77)
+    with acsim.Simulator(cfg, device=0) as g, oracle_mod.OracleSimulator(cfg) as o:
+        assert np.array_equal(g.neighbors(), o.neighbors())
+        assert np.array_equal(g.fault_status(), o.fault_status())
+        assert np.array_equal(bits(g.values(0)), bits(o.values(0)))   # x^0
+
+
+def test_round_chunks_equal_run(oracle_mod):
+    cfg = preset("cfg4_eps", n_nodes=50000, loss_p=0.05, trace_spread=True)
+    with acsim.Simulator(cfg) as a, acsim.Simulator(cfg) as b:
+        a.run()
+        steps = 0
+        while not b.round(3).done:
+            steps += 1
+            assert steps < 1000
+        assert a.rounds().tolist() == b.rounds().tolist()
+        assert np.array_equal(bits(a.values(0)), bits(b.values(0)))
+        assert np.array_equal(bits(a.spread_trace(0)), bits(b.spread_trace(0)))
+
+
+def test_resume_exact():
+    cfg = preset("cfg4_eps", n_nodes=50000, fault_model="byzantine", n_faulty=500,
+                 byz_strategy="random", byz_delta=0.01)
+    with acsim.Simulator(cfg) as a:
+        a.round(5)
+        x5 = a.values(0)
+        a.run()
+        ra, xa = a.rounds().tolist(), a.values(0)
+    with acsim.Simulator(cfg) as b:
+        b.set_state(5, x5)
+        b.run()
+        assert b.rounds().tolist() == ra
+        assert np.array_equal(bits(b.values(0)), bits(xa))
+
+
+def test_deterministic_across_runs():
+    cfg = preset("cfg4", max_rounds=10)
+    outs = []
+    for _ in range(2):
+        with acsim.Simulator(cfg) as s:
+            s.run()
+            outs.append(s.values(0).tobytes())
+    assert outs[0] == outs[1]
+
+
+def test_fixed_mode_runs_exactly_R():
+    cfg = preset("cfg4", n_nodes=1 << 16, max_rounds=37)
+    r = acsim.simulate(cfg)
+    assert r.rounds.tolist() == [37]
+    assert r.node_rounds == 37 * (1 << 16)
+
+
+def test_kernel_timing_counts_round_launches():
+    cfg = preset("cfg4", n_nodes=1 << 16, max_rounds=12)
+    with acsim.Simulator(cfg) as s:
+        s.set_kernel_timing(True)
+        s.run()
+        ms, n, name = s.kernel_timing()
+        assert n == 12 and ms > 0 and name.startswith("k_round_regular<32,5")
