@@ -45,6 +45,7 @@ struct acs_sim {
     uint32_t d = 0, dp = 0;
     Path path = PATH_GENERIC;
     bool clean = true;
+    bool ell_sorted = false;   // rows stored ascending (clean + order-independent rule)
     MsgParams mp{};
     double* x[2] = {nullptr, nullptr};
     uint32_t* ell = nullptr;
@@ -422,6 +423,10 @@ int acs_create(const acs_config* cfg, int backend, const int* devices, int n_dev
         CREATE_TRY(hipMemsetAsync(s->ell, 0, words * sizeof(uint32_t), s->stream));
         const uint64_t gseed = cfg->graph_seed ? cfg->graph_seed : cfg->seed;
         CREATE_TRY(launch_build_ell(s->ell, s->N, s->d, s->dp, make_feistel(s->N, gseed), s->stream));
+        if (s->clean && cfg->rule != ACS_RULE_AVERAGE && s->path == PATH_REGULAR) {
+            CREATE_TRY(launch_sort_ell_rows(s->ell, s->N, s->d, s->stream));
+            s->ell_sorted = true;
+        }
     }
     if (cfg->fault_model != ACS_FAULT_NONE) {
         CREATE_TRY(hipMalloc(&s->status, BN * sizeof(uint32_t)));
@@ -586,8 +591,19 @@ int acs_get_neighbors(acs_sim* s, uint32_t* out, uint64_t n) {
     HIP_TRY(hipSetDevice(s->device));
     const uint64_t words = ((s->N + 63) / 64) * 64ull * s->dp;
     std::vector<uint32_t> h(words);
-    HIP_TRY(hipMemcpyAsync(h.data(), s->ell, words * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
-    HIP_TRY(hipStreamSynchronize(s->stream));
+    if (s->ell_sorted) {   // rows are stored sorted: rebuild the spec (slot) order on the side
+        uint32_t* tmp = nullptr;
+        HIP_TRY(hipMalloc(&tmp, words * sizeof(uint32_t)));
+        const uint64_t gseed = s->c.graph_seed ? s->c.graph_seed : s->c.seed;
+        hipError_t e = launch_build_ell(tmp, s->N, s->d, s->dp, make_feistel(s->N, gseed), s->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(h.data(), tmp, words * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+        (void)hipFree(tmp);
+        HIP_TRY(e);
+    } else {
+        HIP_TRY(hipMemcpyAsync(h.data(), s->ell, words * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+    }
     for (uint64_t i = 0; i < s->N; ++i)
         for (uint32_t t = 0; t < s->d; ++t)
             out[i * s->d + t] = h[(((i >> 6) * (s->dp >> 2) + (t >> 2)) * 64 + (i & 63)) * 4 + (t & 3)];

@@ -76,6 +76,8 @@ hipError_t launch_init_values(double* x, uint64_t B, uint64_t N, Key key, uint64
                               hipStream_t s);
 hipError_t launch_build_ell(uint32_t* ell, uint64_t N, uint32_t d, uint32_t dp, const Feistel& f,
                             hipStream_t s);
+// Sort each ELL row ascending (clean configs with order-independent rules only; d in {4,8,16,32}).
+hipError_t launch_sort_ell_rows(uint32_t* ell, uint64_t N, uint32_t d, hipStream_t s);
 hipError_t build_fault_status(uint32_t* status, uint64_t B, uint64_t N, uint32_t f,
                               uint32_t fault_model, uint32_t crash_window, Key key,
                               uint64_t inst_offset, hipStream_t s);

@@ -54,12 +54,14 @@ __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs
         const double xi = x[i];
         double res = xi;
         bool honest = true, active = true;
-        const uint32_t* stv = nullptr;
+        const uint32_t* stv = nullptr;   // null: loss only, no fault schedule
         if constexpr (!CLEAN) {
-            stv = a.status + lb * N;
-            const uint32_t si = stv[i];
-            honest = si == kHonest;
-            active = is_active(si, a.r);
+            if (a.status) {
+                stv = a.status + lb * N;
+                const uint32_t si = stv[i];
+                honest = si == kHonest;
+                active = is_active(si, a.r);
+            }
         }
         if (active) {
             const uint4* cp = reinterpret_cast<const uint4*>(a.ell) +
@@ -86,10 +88,19 @@ __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs
                 const uint32_t r = a.r;
                 double xj[D];
                 uint32_t sj[D];
+                // all gathers first, unconditionally (the branch is uniform and hoisted)
+                if (stv) {
 #pragma unroll
-                for (int t = 0; t < D; ++t) {   // all gathers first, unconditionally
-                    xj[t] = x[col[t]];
-                    sj[t] = stv[col[t]];
+                    for (int t = 0; t < D; ++t) {
+                        xj[t] = x[col[t]];
+                        sj[t] = stv[col[t]];
+                    }
+                } else {
+#pragma unroll
+                    for (int t = 0; t < D; ++t) {
+                        xj[t] = x[col[t]];
+                        sj[t] = kHonest;
+                    }
                 }
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {

@@ -4,6 +4,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "engine.hpp"
+#include "sortnet.hpp"
 
 namespace acs {
 
@@ -33,6 +34,39 @@ __global__ __launch_bounds__(256) void k_build_ell(uint32_t* ell, uint64_t N, ui
     const uint32_t t0 = 2 * k, t1 = 2 * k + 1;
     ell[base + (uint64_t)(t0 >> 2) * 256 + (t0 & 3)] = fw;
     ell[base + (uint64_t)(t1 >> 2) * 256 + (t1 & 3)] = iv;
+}
+
+// Sort every row of the ELL ascending (rows of D ids, D a compile-time multiple of 4).  Used
+// only for clean configs under order-independent rules (trimmed mean / midpoint / DLPSW sort the
+// received values anyway, and a clean config has no slot-dependent drop or fault decisions), so
+// the round's result is unchanged; the gathers of one wave instruction then fall into a narrow
+// band of x (the t-th smallest neighbour of every lane), which measurably improves L2 reuse.
+template <int D>
+__global__ __launch_bounds__(256) void k_sort_ell_rows(uint32_t* ell, uint64_t N) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= N) return;
+    uint4* cp = reinterpret_cast<uint4*>(ell) + (i >> 6) * (D / 4) * 64 + (i & 63);
+    uint32_t v[D];
+#pragma unroll
+    for (int q = 0; q < D / 4; ++q) {
+        const uint4 c = cp[q * 64];
+        v[4 * q] = c.x; v[4 * q + 1] = c.y; v[4 * q + 2] = c.z; v[4 * q + 3] = c.w;
+    }
+    select_sort<D>(v);
+#pragma unroll
+    for (int q = 0; q < D / 4; ++q) cp[q * 64] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+}
+
+hipError_t launch_sort_ell_rows(uint32_t* ell, uint64_t N, uint32_t d, hipStream_t s) {
+    const dim3 grid((unsigned)((N + 255) / 256));
+    switch (d) {
+        case 4: hipLaunchKernelGGL(k_sort_ell_rows<4>, grid, dim3(256), 0, s, ell, N); break;
+        case 8: hipLaunchKernelGGL(k_sort_ell_rows<8>, grid, dim3(256), 0, s, ell, N); break;
+        case 16: hipLaunchKernelGGL(k_sort_ell_rows<16>, grid, dim3(256), 0, s, ell, N); break;
+        case 32: hipLaunchKernelGGL(k_sort_ell_rows<32>, grid, dim3(256), 0, s, ell, N); break;
+        default: return hipErrorNotSupported;
+    }
+    return hipGetLastError();
 }
 
 __global__ __launch_bounds__(256) void k_fault_keys(uint64_t* keys, uint64_t N, Key key, uint64_t inst_offset) {

@@ -80,11 +80,16 @@ struct SelectNet {
     static constexpr int count = list.n;
 };
 
+__device__ __forceinline__ double ce_min(double a, double b) { return __builtin_fmin(a, b); }
+__device__ __forceinline__ double ce_max(double a, double b) { return __builtin_fmax(a, b); }
+__device__ __forceinline__ uint32_t ce_min(uint32_t a, uint32_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint32_t ce_max(uint32_t a, uint32_t b) { return a < b ? b : a; }
+
 template <int A, int B, typename T, int M>
 __device__ __forceinline__ void cmpx(T (&v)[M]) {
     const T a = v[A], b = v[B];
-    v[A] = __builtin_fmin(a, b);
-    v[B] = __builtin_fmax(a, b);
+    v[A] = ce_min(a, b);
+    v[B] = ce_max(a, b);
 }
 
 template <typename Net, typename T, int M, size_t... I>
