@@ -103,6 +103,10 @@ def _declare(lib: C.CDLL) -> None:
     P = C.POINTER
     sigs = {
         "acs_create": (i32, [P(AcsConfig), i32, P(C.c_int), i32, P(vp)]),
+        "acs_comm_id_size": (i32, []),
+        "acs_get_comm_id": (i32, [vp, u64]),
+        "acs_create_partitioned": (i32, [P(AcsConfig), i32, i32, i32, vp, u64, P(vp)]),
+        "acs_get_partition_values": (i32, [vp, i32, vp, u64]),
         "acs_round": (i32, [vp, u32, P(AcsRoundInfo)]),
         "acs_run": (i32, [vp, P(AcsResult)]),
         "acs_get_values": (i32, [vp, u64, vp, u64]),

@@ -70,6 +70,30 @@ def max_over_ranks(value: float, group=None) -> float:
     return float(t.item())
 
 
+def make_comm_id(rank: int, group=None, src: int = 0) -> bytes:
+    """RCCL unique id created on `src` and broadcast over torch.distributed (gloo or nccl)."""
+    import torch.distributed as dist
+    from . import _abi
+    import ctypes as C
+    obj = [None]
+    if rank == src:
+        lib = _abi.load_library()
+        n = lib.acs_comm_id_size()
+        buf = C.create_string_buffer(n)
+        _abi.check(lib, lib.acs_get_comm_id(buf, n))
+        obj = [buf.raw]
+    dist.broadcast_object_list(obj, src=src, group=group)
+    return obj[0]
+
+
+def partitioned_simulator(cfg: Config, rank: int, world: int, device: int, group=None):
+    """This rank's node partition of one RANDOM_REGULAR instance (cfg5): rows of the graph are
+    split over `world` GPUs, x^{r+1} is all-gathered over RCCL every round."""
+    from .sim import Simulator
+    cid = make_comm_id(rank, group)
+    return Simulator(cfg, device=device, partitions=world, rank=rank, comm_id=cid)
+
+
 def run_sharded(cfg: Config, rank: int, world: int, device: int = 0,
                 sim_factory: Optional[Callable] = None, group=None,
                 return_values: bool = False):

@@ -42,19 +42,31 @@ class Result:
 class Simulator:
     """One device-resident simulation handle (``acs_sim``)."""
 
-    def __init__(self, cfg: Config | str, device: int = 0, backend: str = "hip"):
+    def __init__(self, cfg: Config | str, device: int = 0, backend: str = "hip",
+                 partitions: int = 1, rank: int = 0, comm_id: Optional[bytes] = None):
+        """partitions > 1 node-partitions one RANDOM_REGULAR instance: with
+        comm_id (RCCL unique id from acsim.distributed) this handle is `rank`'s partition on
+        `device`; without it all partitions are simulated on `device` with private x copies
+        (validation mode, see include/acsim.h acs_create_partitioned)."""
         if isinstance(cfg, str):
             cfg = preset(cfg)
         if backend != "hip":
             raise ValueError("acsim implements backend='hip' only; the CPU spec reference is "
                              "test infrastructure (oracle/) and is not a product backend")
         self.cfg = cfg
+        self.partitions = int(partitions)
         self._lib = _abi.load_library()
         self._c = cfg.to_c()
-        devs = (C.c_int * 1)(int(device))
         h = C.c_void_p()
-        _abi.check(self._lib, self._lib.acs_create(C.byref(self._c), _abi.BACKEND_HIP, devs, 1,
-                                                   C.byref(h)))
+        if self.partitions == 1 and comm_id is None:
+            devs = (C.c_int * 1)(int(device))
+            rc = self._lib.acs_create(C.byref(self._c), _abi.BACKEND_HIP, devs, 1, C.byref(h))
+        else:
+            idbuf = None if comm_id is None else C.create_string_buffer(bytes(comm_id), len(comm_id))
+            rc = self._lib.acs_create_partitioned(C.byref(self._c), int(device), self.partitions,
+                                                  int(rank), idbuf, 0 if comm_id is None else len(comm_id),
+                                                  C.byref(h))
+        _abi.check(self._lib, rc)
         self._h = h
 
     # -------------------------------------------------------------------------- lifecycle
@@ -106,6 +118,12 @@ class Simulator:
     def values(self, instance: int = 0) -> np.ndarray:
         out = np.empty(self.N, dtype=np.float64)
         self._chk(self._lib.acs_get_values(self._h, int(instance), out.ctypes.data, out.size))
+        return out
+
+    def partition_values(self, partition: int) -> np.ndarray:
+        """Virtual partitions: the private x copy of one partition."""
+        out = np.empty(self.N, dtype=np.float64)
+        self._chk(self._lib.acs_get_partition_values(self._h, int(partition), out.ctypes.data, out.size))
         return out
 
     def all_values(self) -> np.ndarray:

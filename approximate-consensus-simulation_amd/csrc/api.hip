@@ -1,10 +1,12 @@
 // api.hip — C ABI (include/acsim.h) over the HIP round engine: handle lifecycle, HBM buffer
-// ownership, kernel-path selection, the round-chunk loop with device-side early exit, and the
-// bench-time kernel event timing.  SURVEY §8(b) (C1/C9).
+// ownership, kernel-path selection, the round-chunk loop with device-side early exit, node
+// partitioning with RCCL (cfg5), and the bench-time kernel event timing.  SURVEY §8(b), §8(e).
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
+
+#include <rccl/rccl.h>
 
 #include <chrono>
 #include <string>
@@ -35,7 +37,20 @@ static int fail(int code, const char* fmt, ...) {
                         __FILE__, __LINE__);                                              \
     } while (0)
 
-enum Path { PATH_REGULAR = 0, PATH_GENERIC = 1, PATH_BATCHED = 2 };
+#define NCCL_TRY(expr)                                                                    \
+    do {                                                                                  \
+        ncclResult_t r_ = (expr);                                                         \
+        if (r_ != ncclSuccess)                                                            \
+            return fail(ACS_ECOMM, "%s failed: %s (%s:%d)", #expr, ncclGetErrorString(r_), \
+                        __FILE__, __LINE__);                                              \
+    } while (0)
+
+enum Path { PATH_REGULAR = 0, PATH_GENERIC = 1, PATH_BATCHED = 2, PATH_DENSE = 3 };
+
+struct Part {              // one node partition's private copy (virtual partitions only)
+    double* x[2] = {nullptr, nullptr};
+    uint32_t* ell = nullptr;
+};
 
 struct acs_sim {
     acs_config c{};
@@ -45,10 +60,10 @@ struct acs_sim {
     uint32_t d = 0, dp = 0;
     Path path = PATH_GENERIC;
     bool clean = true;
-    bool ell_sorted = false;   // rows stored ascending (clean + order-independent rule)
+    bool ell_sorted = false;       // rows stored ascending (clean + order-independent rule)
     MsgParams mp{};
     double* x[2] = {nullptr, nullptr};
-    uint32_t* ell = nullptr;
+    uint32_t* ell = nullptr;       // rows [row0, row0 + rows_per) of this rank
     uint32_t* status = nullptr;
     InstState* st = nullptr;
     double2* partial = nullptr;
@@ -58,6 +73,16 @@ struct acs_sim {
     uint32_t* h_ndone = nullptr;   // pinned [2]
     uint32_t round = 0;            // round of every unfinished instance
     bool all_done = false;
+    // node partitioning: rank owns rows [rank*rows_per, (rank+1)*rows_per) ∩ [0, N)
+    int nranks = 1, rank = 0;
+    bool partitioned = false;      // node partition mode (virtual, or RCCL with >= 1 rank)
+    bool virt = false;             // all nranks partitions simulated on this device
+    uint64_t rows_per = 0, Npad = 0;
+    ncclComm_t comm = nullptr;
+    double2* gpart = nullptr;      // (-min, max) exchanged by all-reduce
+    double* dsorted = nullptr;     // dense path: sorted base multiset [N]
+    uint32_t* dcounts = nullptr;   // dense path: |B|, #Byzantine, #crash-silent
+    std::vector<Part> parts;       // virtual partitions 1..P-1 (partition 0 uses x / ell)
     // kernel timing (bench)
     bool timing = false;
     std::vector<hipEvent_t> ev;    // pairs (start, stop)
@@ -142,13 +167,22 @@ static void release(acs_sim* s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
+    if (s->comm) (void)ncclCommDestroy(s->comm);
     for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
+    for (Part& p : s->parts) {
+        (void)hipFree(p.x[0]);
+        (void)hipFree(p.x[1]);
+        (void)hipFree(p.ell);
+    }
     (void)hipFree(s->x[0]);
     (void)hipFree(s->x[1]);
     (void)hipFree(s->ell);
     (void)hipFree(s->status);
     (void)hipFree(s->st);
     (void)hipFree(s->partial);
+    (void)hipFree(s->gpart);
+    (void)hipFree(s->dsorted);
+    (void)hipFree(s->dcounts);
     (void)hipFree(s->n_done);
     (void)hipFree(s->trace);
     if (s->h_ndone) (void)hipHostFree(s->h_ndone);
@@ -156,10 +190,11 @@ static void release(acs_sim* s) {
     delete s;
 }
 
-static FinalizeArgs make_finalize(acs_sim* s, uint32_t r_next, uint32_t nblk, bool init) {
+static FinalizeArgs make_finalize(acs_sim* s, uint32_t r_next, const double2* partial, uint32_t nblk,
+                                  bool init) {
     FinalizeArgs f{};
     f.st = s->st;
-    f.partial = s->partial;
+    f.partial = partial;
     f.nblk = nblk;
     f.r_next = r_next;
     f.max_rounds = s->c.max_rounds;
@@ -172,11 +207,19 @@ static FinalizeArgs make_finalize(acs_sim* s, uint32_t r_next, uint32_t nblk, bo
     return f;
 }
 
-// (Re)initialise the per-instance state from x[round & 1] (create and set_state).
+static uint64_t part_row0(const acs_sim* s, int p) { return (uint64_t)p * s->rows_per; }
+static uint64_t part_rows(const acs_sim* s, int p) {
+    const uint64_t r0 = part_row0(s, p);
+    if (r0 >= s->N) return 0;
+    return s->N - r0 < s->rows_per ? s->N - r0 : s->rows_per;
+}
+
+// (Re)initialise the per-instance state from x[round & 1] (create and set_state).  Every rank
+// holds the full x, so the initial honest min/max needs no exchange.
 static int init_state(acs_sim* s, uint32_t round) {
     HIP_TRY(hipMemsetAsync(s->n_done, 0, sizeof(uint32_t), s->stream));
     HIP_TRY(launch_partials_from_x(s->x[round & 1u], s->status, s->B, s->N, s->partial, s->nblk_init, s->stream));
-    const FinalizeArgs f = make_finalize(s, round, s->nblk_init, true);
+    const FinalizeArgs f = make_finalize(s, round, s->partial, s->nblk_init, true);
     HIP_TRY(launch_finalize(f, s->B, s->stream));
     HIP_TRY(hipMemcpyAsync(s->h_ndone, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
@@ -207,7 +250,21 @@ static int harvest_timing(acs_sim* s) {
     return ACS_OK;
 }
 
-static int enqueue_round(acs_sim* s, uint32_t r) {
+static int timing_begin(acs_sim* s, hipEvent_t* e1) {
+    *e1 = nullptr;
+    if (!s->timing) return ACS_OK;
+    if (s->ev_used + 2 > 4096) {
+        int rc = harvest_timing(s);
+        if (rc) return rc;
+    }
+    hipEvent_t e0 = next_event(s);
+    *e1 = next_event(s);
+    if (!e0 || !*e1) return fail(ACS_EDEVICE, "hipEventCreate failed");
+    HIP_TRY(hipEventRecord(e0, s->stream));
+    return ACS_OK;
+}
+
+static RoundArgs round_args(acs_sim* s, uint32_t r) {
     RoundArgs a{};
     a.xin = s->x[r & 1u];
     a.xout = s->x[(r + 1) & 1u];
@@ -216,6 +273,8 @@ static int enqueue_round(acs_sim* s, uint32_t r) {
     a.st = s->st;
     a.partial = s->partial;
     a.N = s->N;
+    a.row0 = 0;
+    a.nrows = s->N;
     a.m = (uint32_t)s->m;
     a.d = s->d;
     a.dp = s->dp;
@@ -225,24 +284,94 @@ static int enqueue_round(acs_sim* s, uint32_t r) {
     a.r = r;
     a.nblk = s->nblk;
     a.mp = s->mp;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (s->timing) {
-        if (s->ev_used + 2 > 4096) {
-            int rc = harvest_timing(s);
-            if (rc) return rc;
+    return a;
+}
+
+// One round x^r -> x^{r+1}: round kernel(s), [exchange], spread finalize.
+static int enqueue_round(acs_sim* s, uint32_t r) {
+    RoundArgs a = round_args(s, r);
+    hipEvent_t e1;
+    int rc = timing_begin(s, &e1);
+    if (rc) return rc;
+    if (!s->partitioned) {
+        if (s->path == PATH_REGULAR) {
+            HIP_TRY(launch_round_regular(a, s->B, s->clean, s->stream));
+        } else if (s->path == PATH_DENSE) {
+            DenseArgs d{};
+            d.x = a.xin;
+            d.xo = a.xout;
+            d.status = s->status;
+            d.st = s->st;
+            d.partial = s->partial;
+            d.sorted = s->dsorted;
+            d.counts = s->dcounts;
+            d.N = (uint32_t)s->N;
+            uint32_t P = 1;
+            while (P < s->N) P <<= 1;
+            d.P = P;
+            d.r = r;
+            d.rule = s->c.rule;
+            d.trim = s->c.trim;
+            d.byz = s->c.byz_strategy;
+            d.delta = s->mp.delta;
+            d.bconst = s->mp.bconst;
+            HIP_TRY(launch_round_dense(d, s->stream));
+        } else {
+            HIP_TRY(launch_round_generic(a, s->B, s->stream));
         }
-        e0 = next_event(s);
-        e1 = next_event(s);
-        if (!e0 || !e1) return fail(ACS_EDEVICE, "hipEventCreate failed");
-        HIP_TRY(hipEventRecord(e0, s->stream));
+        if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
+        HIP_TRY(launch_finalize(make_finalize(s, r + 1, s->partial, s->nblk, false), s->B, s->stream));
+        return ACS_OK;
     }
-    if (s->path == PATH_REGULAR)
-        HIP_TRY(launch_round_regular(a, s->B, s->clean, s->stream));
-    else
-        HIP_TRY(launch_round_generic(a, s->B, s->stream));
-    if (s->timing) HIP_TRY(hipEventRecord(e1, s->stream));
-    const FinalizeArgs f = make_finalize(s, r + 1, s->nblk, false);
-    HIP_TRY(launch_finalize(f, s->B, s->stream));
+    if (s->virt) {
+        // every partition p reads its own full copy, writes its own rows; block partials of
+        // partition p land at partial[p * nblk]
+        for (int p = 0; p < s->nranks; ++p) {
+            RoundArgs ap = a;
+            if (p > 0) {
+                ap.xin = s->parts[p - 1].x[r & 1u];
+                ap.xout = s->parts[p - 1].x[(r + 1) & 1u];
+                ap.ell = s->parts[p - 1].ell;
+            }
+            ap.row0 = part_row0(s, p);
+            ap.nrows = part_rows(s, p);
+            ap.partial = s->partial + (uint64_t)p * s->nblk;
+            if (ap.nrows == 0) continue;   // empty tail partition (its partials are not folded)
+            HIP_TRY(launch_round_regular(ap, s->B, s->clean, s->stream));
+        }
+        if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
+        // all-gather emulation: copy each partition's fresh rows into every other copy
+        const uint32_t o = (r + 1) & 1u;
+        for (int p = 0; p < s->nranks; ++p) {
+            const uint64_t r0 = part_row0(s, p), nr = part_rows(s, p);
+            if (!nr) continue;
+            const double* src = p == 0 ? s->x[o] : s->parts[p - 1].x[o];
+            for (int q = 0; q < s->nranks; ++q) {
+                if (q == p) continue;
+                double* dst = q == 0 ? s->x[o] : s->parts[q - 1].x[o];
+                HIP_TRY(hipMemcpyAsync(dst + r0, src + r0, nr * sizeof(double), hipMemcpyDeviceToDevice, s->stream));
+            }
+        }
+        uint32_t nblk_live = 0;
+        for (int p = 0; p < s->nranks; ++p)
+            if (part_rows(s, p)) nblk_live = (uint32_t)((p + 1) * s->nblk);
+        HIP_TRY(launch_finalize(make_finalize(s, r + 1, s->partial, nblk_live, false), s->B, s->stream));
+        return ACS_OK;
+    }
+    // RCCL partition: own rows, then in-place all-gather of x^{r+1} and all-reduce of the spread
+    a.row0 = part_row0(s, s->rank);
+    a.nrows = part_rows(s, s->rank);
+    if (a.nrows) HIP_TRY(launch_round_regular(a, s->B, s->clean, s->stream));
+    if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
+    double* xo = s->x[(r + 1) & 1u];
+    NCCL_TRY(ncclAllGather(xo + a.row0, xo, s->rows_per, ncclFloat64, s->comm, s->stream));
+    FinalizeArgs fold = make_finalize(s, r + 1, s->partial, a.nrows ? s->nblk : 0, false);
+    fold.fold_out = s->gpart;
+    HIP_TRY(launch_finalize(fold, s->B, s->stream));
+    NCCL_TRY(ncclAllReduce(s->gpart, s->gpart, 2, ncclFloat64, ncclMax, s->comm, s->stream));
+    FinalizeArgs fin = make_finalize(s, r + 1, s->gpart, 1, false);
+    fin.negmin = 1;
+    HIP_TRY(launch_finalize(fin, s->B, s->stream));
     return ACS_OK;
 }
 
@@ -277,15 +406,11 @@ static int advance(acs_sim* s, uint32_t k) {
         a.term_eps = s->c.termination == ACS_TERM_EPS;
         a.eps = s->c.eps;
         a.mp = s->mp;
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (s->timing) {
-            e0 = next_event(s);
-            e1 = next_event(s);
-            if (!e0 || !e1) return fail(ACS_EDEVICE, "hipEventCreate failed");
-            HIP_TRY(hipEventRecord(e0, s->stream));
-        }
+        hipEvent_t e1;
+        int rc = timing_begin(s, &e1);
+        if (rc) return rc;
         HIP_TRY(launch_batched_small(a, s->B, k, s->stream));
-        if (s->timing) HIP_TRY(hipEventRecord(e1, s->stream));
+        if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
         HIP_TRY(hipMemcpyAsync(s->h_ndone, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(hipStreamSynchronize(s->stream));
         s->round += k;
@@ -326,30 +451,42 @@ static int advance(acs_sim* s, uint32_t k) {
     return ACS_OK;
 }
 
-// ------------------------------------------------------------------------- C ABI
-extern "C" {
+// Build the adjacency rows of partition p into `ell` (sorted when the config allows it).
+static hipError_t build_rows(acs_sim* s, uint32_t* ell, int p) {
+    const uint64_t gseed = s->c.graph_seed ? s->c.graph_seed : s->c.seed;
+    const uint64_t nr = !s->partitioned ? s->N : part_rows(s, p);
+    if (nr == 0) return hipSuccess;
+    hipError_t e = launch_build_ell(ell, s->N, !s->partitioned ? 0 : part_row0(s, p), nr, s->d, s->dp,
+                                    make_feistel(s->N, gseed), s->stream);
+    if (e == hipSuccess && s->ell_sorted) e = launch_sort_ell_rows(ell, nr, s->d, s->stream);
+    return e;
+}
 
-int acs_abi_version(void) { return ACS_ABI_VERSION; }
-
-const char* acs_last_error(void) { return g_err.c_str(); }
-
-int acs_create(const acs_config* cfg, int backend, const int* devices, int n_devices, acs_sim** out) {
+static int create_impl(const acs_config* cfg, int device, int nranks, int rank, const void* comm_id,
+                       uint64_t id_len, acs_sim** out) {
     if (!out) return fail(ACS_EINVAL, "null out");
     *out = nullptr;
     int rc = validate(cfg);
     if (rc) return rc;
-    if (backend != ACS_HIP)
-        return fail(ACS_EUNSUPPORTED, "libacsim implements ACS_HIP only (the CPU spec reference is the "
-                                      "test oracle in oracle/, not a product backend)");
-    if (n_devices != 1 || !devices)
-        return fail(ACS_EINVAL, "exactly one device per handle (shard across processes, one rank per GPU)");
+    if (nranks < 1 || rank < 0 || rank >= nranks) return fail(ACS_EINVAL, "bad rank / n_ranks");
+    const bool partitioned = nranks > 1 || comm_id != nullptr;
+    const bool virt = partitioned && !comm_id;
+    if (virt && rank != 0) return fail(ACS_EINVAL, "virtual partitions live on one handle (rank 0)");
+    if (comm_id && id_len != sizeof(ncclUniqueId))
+        return fail(ACS_EINVAL, "comm id must be %zu bytes", sizeof(ncclUniqueId));
+    if (partitioned) {
+        if (cfg->topology != ACS_TOPO_RANDOM_REGULAR || cfg->n_instances != 1 ||
+            !regular_fast_supported(cfg->degree, cfg->trim, cfg->rule))
+            return fail(ACS_EUNSUPPORTED, "node partitioning needs one RANDOM_REGULAR instance with a "
+                                          "compiled (degree, trim) variant");
+    }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(ACS_EDEVICE, "no HIP device");
-    if (devices[0] < 0 || devices[0] >= ndev) return fail(ACS_EINVAL, "device %d out of range", devices[0]);
+    if (device < 0 || device >= ndev) return fail(ACS_EINVAL, "device %d out of range", device);
 
     acs_sim* s = new acs_sim();
     s->c = *cfg;
-    s->device = devices[0];
+    s->device = device;
     s->N = cfg->n_nodes;
     s->B = cfg->n_instances;
     s->m = cfg->topology == ACS_TOPO_COMPLETE ? s->N : (uint64_t)cfg->degree + 1;
@@ -364,10 +501,20 @@ int acs_create(const acs_config* cfg, int backend, const int* devices, int n_dev
     s->mp.inst_offset = cfg->instance_offset;
     s->mp.delta = cfg->byz_delta;
     s->mp.bconst = cfg->byz_const + 0.0;   // canonicalise -0.0 (no -0 ever enters a sort)
+    s->nranks = nranks;
+    s->partitioned = partitioned;
+    s->rank = rank;
+    s->virt = virt;
+    s->rows_per = partitioned ? ((s->N + nranks - 1) / nranks + 63) / 64 * 64 : s->N;
+    s->Npad = partitioned ? s->rows_per * nranks : s->N;
 
     if (cfg->topology == ACS_TOPO_COMPLETE && s->N <= kBatchedMaxN) {
         s->path = PATH_BATCHED;
         s->kname = batched_small_name((uint32_t)s->N, cfg->rule);
+    } else if (cfg->topology == ACS_TOPO_COMPLETE && s->B == 1 && !partitioned &&
+               dense_supported(cfg->fault_model, cfg->byz_strategy, cfg->rule, s->mp.thr, s->N)) {
+        s->path = PATH_DENSE;
+        s->kname = "k_dense_sort+k_dense_recv";
     } else if (cfg->topology == ACS_TOPO_RANDOM_REGULAR && regular_fast_supported(s->d, cfg->trim, cfg->rule)) {
         s->path = PATH_REGULAR;
         s->kname = regular_fast_name(s->d, cfg->trim, s->clean);
@@ -384,11 +531,16 @@ int acs_create(const acs_config* cfg, int backend, const int* devices, int n_dev
         delete s;
         return fail(ACS_EUNSUPPORTED, "fault schedules need B*N < 2^31");
     }
-    s->nblk = s->path == PATH_REGULAR ? (uint32_t)((s->N + kRegularBlock - 1) / kRegularBlock)
-                                      : (s->path == PATH_GENERIC ? (uint32_t)s->N : 0u);
+    s->ell_sorted = s->path == PATH_REGULAR && s->clean && cfg->rule != ACS_RULE_AVERAGE;
+    const uint64_t rows_local = partitioned ? s->rows_per : s->N;
+    s->nblk = s->path == PATH_REGULAR ? (uint32_t)((rows_local + kRegularBlock - 1) / kRegularBlock)
+            : s->path == PATH_GENERIC ? (uint32_t)s->N
+            : s->path == PATH_DENSE   ? dense_nblk(s->N)
+                                      : 0u;
     s->nblk_init = (uint32_t)((s->N + 255) / 256);
     if (s->nblk_init > 1024) s->nblk_init = 1024;
-    const uint32_t ncap = s->nblk > s->nblk_init ? s->nblk : s->nblk_init;
+    const uint64_t nround = (uint64_t)s->nblk * (virt ? nranks : 1);
+    const uint64_t ncap = nround > s->nblk_init ? nround : s->nblk_init;
 
 #define CREATE_TRY(expr)                                                                      \
     do {                                                                                      \
@@ -404,12 +556,17 @@ int acs_create(const acs_config* cfg, int backend, const int* devices, int n_dev
 
     CREATE_TRY(hipSetDevice(s->device));
     CREATE_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-    const uint64_t BN = s->B * s->N;
-    CREATE_TRY(hipMalloc(&s->x[0], BN * sizeof(double)));
-    CREATE_TRY(hipMalloc(&s->x[1], BN * sizeof(double)));
+    const uint64_t xlen = s->B * s->Npad;
+    CREATE_TRY(hipMalloc(&s->x[0], xlen * sizeof(double)));
+    CREATE_TRY(hipMalloc(&s->x[1], xlen * sizeof(double)));
     CREATE_TRY(hipMalloc(&s->st, s->B * sizeof(InstState)));
     CREATE_TRY(hipMemsetAsync(s->st, 0, s->B * sizeof(InstState), s->stream));
-    CREATE_TRY(hipMalloc(&s->partial, s->B * (uint64_t)ncap * sizeof(double2)));
+    CREATE_TRY(hipMalloc(&s->partial, s->B * ncap * sizeof(double2)));
+    CREATE_TRY(hipMalloc(&s->gpart, sizeof(double2)));
+    if (s->path == PATH_DENSE) {
+        CREATE_TRY(hipMalloc(&s->dsorted, s->N * sizeof(double)));
+        CREATE_TRY(hipMalloc(&s->dcounts, 4 * sizeof(uint32_t)));
+    }
     CREATE_TRY(hipMalloc(&s->n_done, sizeof(uint32_t)));
     CREATE_TRY(hipHostMalloc(&s->h_ndone, 2 * sizeof(uint32_t), hipHostMallocDefault));
     if (cfg->trace_spread) {
@@ -418,23 +575,40 @@ int acs_create(const acs_config* cfg, int backend, const int* devices, int n_dev
         CREATE_TRY(hipMemsetAsync(s->trace, 0xFF, nt * sizeof(double), s->stream));   // NaN
     }
     if (cfg->topology == ACS_TOPO_RANDOM_REGULAR) {
-        const uint64_t words = ((s->N + 63) / 64) * 64ull * s->dp;
+        const uint64_t words = ((rows_local + 63) / 64) * 64ull * s->dp;
         CREATE_TRY(hipMalloc(&s->ell, words * sizeof(uint32_t)));
         CREATE_TRY(hipMemsetAsync(s->ell, 0, words * sizeof(uint32_t), s->stream));
-        const uint64_t gseed = cfg->graph_seed ? cfg->graph_seed : cfg->seed;
-        CREATE_TRY(launch_build_ell(s->ell, s->N, s->d, s->dp, make_feistel(s->N, gseed), s->stream));
-        if (s->clean && cfg->rule != ACS_RULE_AVERAGE && s->path == PATH_REGULAR) {
-            CREATE_TRY(launch_sort_ell_rows(s->ell, s->N, s->d, s->stream));
-            s->ell_sorted = true;
+        CREATE_TRY(build_rows(s, s->ell, partitioned ? rank : 0));
+        if (virt) {
+            s->parts.resize(nranks - 1);
+            for (int p = 1; p < nranks; ++p) {
+                Part& q = s->parts[p - 1];
+                CREATE_TRY(hipMalloc(&q.x[0], xlen * sizeof(double)));
+                CREATE_TRY(hipMalloc(&q.x[1], xlen * sizeof(double)));
+                CREATE_TRY(hipMalloc(&q.ell, words * sizeof(uint32_t)));
+                CREATE_TRY(hipMemsetAsync(q.ell, 0, words * sizeof(uint32_t), s->stream));
+                CREATE_TRY(build_rows(s, q.ell, p));
+            }
         }
     }
     if (cfg->fault_model != ACS_FAULT_NONE) {
-        CREATE_TRY(hipMalloc(&s->status, BN * sizeof(uint32_t)));
+        CREATE_TRY(hipMalloc(&s->status, s->B * s->N * sizeof(uint32_t)));
         CREATE_TRY(build_fault_status(s->status, s->B, s->N, cfg->n_faulty, cfg->fault_model,
                                       cfg->crash_window, s->mp.key, cfg->instance_offset, s->stream));
     }
     CREATE_TRY(launch_init_values(s->x[0], s->B, s->N, s->mp.key, cfg->instance_offset, s->stream));
+    for (Part& q : s->parts) CREATE_TRY(launch_init_values(q.x[0], s->B, s->N, s->mp.key, cfg->instance_offset, s->stream));
 #undef CREATE_TRY
+    if (comm_id) {
+        ncclUniqueId id;
+        memcpy(&id, comm_id, sizeof id);
+        ncclResult_t nr = ncclCommInitRank(&s->comm, nranks, id, rank);
+        if (nr != ncclSuccess) {
+            fail(ACS_ECOMM, "ncclCommInitRank(%d ranks, rank %d) failed: %s", nranks, rank, ncclGetErrorString(nr));
+            release(s);
+            return ACS_ECOMM;
+        }
+    }
     rc = init_state(s, 0);
     if (rc) {
         release(s);
@@ -444,9 +618,44 @@ int acs_create(const acs_config* cfg, int backend, const int* devices, int n_dev
     return ACS_OK;
 }
 
+// ------------------------------------------------------------------------- C ABI
+extern "C" {
+
+int acs_abi_version(void) { return ACS_ABI_VERSION; }
+
+const char* acs_last_error(void) { return g_err.c_str(); }
+
+int acs_create(const acs_config* cfg, int backend, const int* devices, int n_devices, acs_sim** out) {
+    if (out) *out = nullptr;
+    int rc = validate(cfg);
+    if (rc) return rc;
+    if (backend != ACS_HIP)
+        return fail(ACS_EUNSUPPORTED, "libacsim implements ACS_HIP only (the CPU spec reference is the "
+                                      "test oracle in oracle/, not a product backend)");
+    if (n_devices != 1 || !devices)
+        return fail(ACS_EINVAL, "exactly one device per handle (shard across processes, one rank per GPU)");
+    return create_impl(cfg, devices[0], 1, 0, nullptr, 0, out);
+}
+
+int acs_comm_id_size(void) { return (int)sizeof(ncclUniqueId); }
+
+int acs_get_comm_id(void* out, uint64_t n) {
+    if (!out || n < sizeof(ncclUniqueId)) return fail(ACS_EINVAL, "buffer must hold %zu bytes", sizeof(ncclUniqueId));
+    ncclUniqueId id;
+    NCCL_TRY(ncclGetUniqueId(&id));
+    memcpy(out, &id, sizeof id);
+    return ACS_OK;
+}
+
+int acs_create_partitioned(const acs_config* cfg, int device, int n_ranks, int rank, const void* comm_id,
+                           uint64_t id_len, acs_sim** out) {
+    return create_impl(cfg, device, n_ranks, rank, comm_id, id_len, out);
+}
+
 void acs_destroy(acs_sim* s) { release(s); }
 
 static void fill_info(acs_sim* s, const std::vector<InstState>& v, acs_round_info* out) {
+    (void)s;
     if (!out) return;
     memset(out, 0, sizeof *out);
     uint64_t nd = 0;
@@ -516,8 +725,21 @@ int acs_get_values(acs_sim* s, uint64_t b, void* out, uint64_t n) {
     InstState e;
     HIP_TRY(hipMemcpyAsync(&e, s->st + b, sizeof e, hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
-    HIP_TRY(hipMemcpyAsync(out, s->x[e.rounds & 1u] + b * s->N, s->N * sizeof(double), hipMemcpyDeviceToHost,
+    HIP_TRY(hipMemcpyAsync(out, s->x[e.rounds & 1u] + b * s->Npad, s->N * sizeof(double), hipMemcpyDeviceToHost,
                            s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return ACS_OK;
+}
+
+int acs_get_partition_values(acs_sim* s, int partition, void* out, uint64_t n) {
+    if (!s || !out || n < s->N) return fail(ACS_EINVAL, "bad arguments");
+    if (partition < 0 || partition >= (s->virt ? s->nranks : 1)) return fail(ACS_EINVAL, "no such partition copy");
+    HIP_TRY(hipSetDevice(s->device));
+    InstState e;
+    HIP_TRY(hipMemcpyAsync(&e, s->st, sizeof e, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    const double* src = partition == 0 ? s->x[e.rounds & 1u] : s->parts[partition - 1].x[e.rounds & 1u];
+    HIP_TRY(hipMemcpyAsync(out, src, s->N * sizeof(double), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     return ACS_OK;
 }
@@ -568,7 +790,14 @@ int acs_set_state(acs_sim* s, uint32_t round, const void* x, uint64_t n) {
     if (!s || !x || n != s->B * s->N) return fail(ACS_EINVAL, "set_state needs B*N values");
     if (round > s->c.max_rounds) return fail(ACS_EINVAL, "round > max_rounds");
     HIP_TRY(hipSetDevice(s->device));
-    HIP_TRY(hipMemcpyAsync(s->x[round & 1u], x, n * sizeof(double), hipMemcpyHostToDevice, s->stream));
+    const double* hx = (const double*)x;
+    for (uint64_t b = 0; b < s->B; ++b) {
+        HIP_TRY(hipMemcpyAsync(s->x[round & 1u] + b * s->Npad, hx + b * s->N, s->N * sizeof(double),
+                               hipMemcpyHostToDevice, s->stream));
+        for (Part& q : s->parts)
+            HIP_TRY(hipMemcpyAsync(q.x[round & 1u] + b * s->Npad, hx + b * s->N, s->N * sizeof(double),
+                                   hipMemcpyHostToDevice, s->stream));
+    }
     return init_state(s, round);
 }
 
@@ -589,21 +818,18 @@ int acs_get_neighbors(acs_sim* s, uint32_t* out, uint64_t n) {
     if (!s->ell) return fail(ACS_EINVAL, "not a RANDOM_REGULAR topology");
     if (n < s->N * s->d) return fail(ACS_EINVAL, "buffer too small");
     HIP_TRY(hipSetDevice(s->device));
+    // always rebuild the full graph in spec (slot) order on the side: the handle's own ELL may be
+    // sorted and may hold only this rank's rows
     const uint64_t words = ((s->N + 63) / 64) * 64ull * s->dp;
     std::vector<uint32_t> h(words);
-    if (s->ell_sorted) {   // rows are stored sorted: rebuild the spec (slot) order on the side
-        uint32_t* tmp = nullptr;
-        HIP_TRY(hipMalloc(&tmp, words * sizeof(uint32_t)));
-        const uint64_t gseed = s->c.graph_seed ? s->c.graph_seed : s->c.seed;
-        hipError_t e = launch_build_ell(tmp, s->N, s->d, s->dp, make_feistel(s->N, gseed), s->stream);
-        if (e == hipSuccess) e = hipMemcpyAsync(h.data(), tmp, words * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
-        (void)hipFree(tmp);
-        HIP_TRY(e);
-    } else {
-        HIP_TRY(hipMemcpyAsync(h.data(), s->ell, words * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
-        HIP_TRY(hipStreamSynchronize(s->stream));
-    }
+    uint32_t* tmp = nullptr;
+    HIP_TRY(hipMalloc(&tmp, words * sizeof(uint32_t)));
+    const uint64_t gseed = s->c.graph_seed ? s->c.graph_seed : s->c.seed;
+    hipError_t e = launch_build_ell(tmp, s->N, 0, s->N, s->d, s->dp, make_feistel(s->N, gseed), s->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(h.data(), tmp, words * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    (void)hipFree(tmp);
+    HIP_TRY(e);
     for (uint64_t i = 0; i < s->N; ++i)
         for (uint32_t t = 0; t < s->d; ++t)
             out[i * s->d + t] = h[(((i >> 6) * (s->dp >> 2) + (t >> 2)) * 64 + (i & 63)) * 4 + (t & 3)];

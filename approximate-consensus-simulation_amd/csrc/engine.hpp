@@ -31,11 +31,12 @@ struct InstState {
 struct RoundArgs {
     const double* xin;        // x^r, instance-major [B][N]
     double* xout;             // x^{r+1}
-    const uint32_t* ell;      // RANDOM_REGULAR adjacency (see layout above)
+    const uint32_t* ell;      // RANDOM_REGULAR adjacency of rows [row0, row0+nrows) (see layout above)
     const uint32_t* status;   // [B][N] or nullptr when there are no faults
     InstState* st;            // [B]
     double2* partial;         // [B][nblk]
     uint64_t N;
+    uint64_t row0, nrows;     // receivers handled by this launch (node partition; 0, N otherwise)
     uint32_t m;               // entries per receiver
     uint32_t d, dp;           // degree, degree rounded up to 4
     uint32_t topology, rule, trim;
@@ -56,6 +57,8 @@ struct FinalizeArgs {
     uint64_t trace_stride;    // max_rounds + 1
     uint32_t* n_done;
     uint32_t init_mode;       // 1: (re)initialisation, ignores the done flag
+    uint32_t negmin;          // 1: partial[k].x holds -min (after an all-reduce MAX of (-min, max))
+    double2* fold_out;        // non-null: only fold the partials into (-min, max) here (node partition)
 };
 
 struct BatchArgs {
@@ -74,8 +77,8 @@ struct BatchArgs {
 // ---- setup kernels (setup.hip)
 hipError_t launch_init_values(double* x, uint64_t B, uint64_t N, Key key, uint64_t inst_offset,
                               hipStream_t s);
-hipError_t launch_build_ell(uint32_t* ell, uint64_t N, uint32_t d, uint32_t dp, const Feistel& f,
-                            hipStream_t s);
+hipError_t launch_build_ell(uint32_t* ell, uint64_t N, uint64_t row0, uint64_t nrows, uint32_t d, uint32_t dp,
+                            const Feistel& f, hipStream_t s);
 // Sort each ELL row ascending (clean configs with order-independent rules only; d in {4,8,16,32}).
 hipError_t launch_sort_ell_rows(uint32_t* ell, uint64_t N, uint32_t d, hipStream_t s);
 hipError_t build_fault_status(uint32_t* status, uint64_t B, uint64_t N, uint32_t f,
@@ -98,6 +101,23 @@ constexpr uint32_t kRegularBlock = 256;
 // Generic kernel: one workgroup per receiver, LDS bitonic sort (any topology, m <= 8192).
 constexpr uint32_t kGenericMaxM = 8192;
 hipError_t launch_round_generic(const RoundArgs& a, uint64_t B, hipStream_t s);
+
+// Dense shared-sort kernels (round_dense.hip): COMPLETE topology, no loss, sort-based rule,
+// no crash faults, Byzantine SPLIT/CONSTANT; one instance.
+struct DenseArgs {
+    const double* x;          // x^r
+    double* xo;               // x^{r+1}
+    const uint32_t* status;   // [N] or nullptr
+    InstState* st;
+    double2* partial;         // [dense_nblk(N)]
+    double* sorted;           // [N] scratch: sorted base multiset
+    uint32_t* counts;         // [3] scratch: |B|, #Byzantine, #crash-silent
+    uint32_t N, P, r, rule, trim, byz;
+    double delta, bconst;
+};
+bool dense_supported(uint32_t fault_model, uint32_t byz, uint32_t rule, uint32_t thr, uint64_t N);
+uint32_t dense_nblk(uint64_t N);
+hipError_t launch_round_dense(const DenseArgs& a, hipStream_t s);
 
 // Persistent batched kernel: COMPLETE topology with N <= 64, one wavefront per instance,
 // state in VGPRs across rounds.

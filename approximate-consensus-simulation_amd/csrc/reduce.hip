@@ -38,7 +38,7 @@ __global__ __launch_bounds__(kReduceBlock) void k_finalize(const FinalizeArgs a)
     double mn = kInf, mx = -kInf;
     for (uint32_t k = threadIdx.x; k < a.nblk; k += kReduceBlock) {
         const double2 v = p[k];
-        mn = __builtin_fmin(mn, v.x);
+        mn = __builtin_fmin(mn, a.negmin ? -v.x : v.x);
         mx = __builtin_fmax(mx, v.y);
     }
     __shared__ double2 red[kReduceBlock / 64];
@@ -54,6 +54,10 @@ __global__ __launch_bounds__(kReduceBlock) void k_finalize(const FinalizeArgs a)
         }
         mn = __builtin_fmin(mn, red[0].x);
         mx = __builtin_fmax(mx, red[0].y);
+        if (a.fold_out) {   // node partition: hand (-min, max) to the all-reduce
+            *a.fold_out = make_double2(-mn, mx);
+            return;
+        }
         const double spread = mx - mn;
         S->lo = mn;
         S->hi = mx;

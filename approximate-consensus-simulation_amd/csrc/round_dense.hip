@@ -1,0 +1,207 @@
+// round_dense.hip — complete-graph rounds with one shared sort per round (cfg2 shape).
+//
+// On a complete graph without message loss, every active receiver i sees the same base multiset
+// B = { x_j : j honest or crash-active } (its own entry x_i is one of them) plus receiver-specific
+// constant blocks: n_byz copies of its Byzantine value c_i (SPLIT: hi^r+Δ / lo^r−Δ by receiver
+// parity; CONSTANT: c) and n_silent copies of x_i (crash-silent senders, missing -> x_i).  So:
+//   k_dense_sort  : one workgroup sorts B once per round (LDS bitonic, +inf padding) and counts
+//                   the silent / Byzantine senders;
+//   k_dense_recv  : one wavefront per receiver reads its window R = M[t, m-t) of the merged
+//                   sequence M = B ⊕ {c_i}^n_byz ⊕ {x_i}^n_silent directly by index arithmetic
+//                   (two ranks found by binary search), and applies the rule with the §A.7
+//                   stride-halving tree sum, spread over the wavefront's 64 lanes.
+// The sorted value sequence of S_i is unique (no -0, no NaN), so this equals sorting S_i per
+// receiver (the generic kernel) bit for bit, at O(N log^2 N + N·|R|/64) instead of
+// O(N^2 log^2 N) work per round.  Rounds in which a crash sender delivers partially (r == r_v),
+// message loss, AVERAGE and RANDOM Byzantine values keep the generic kernel.
+#include "resolve.hpp"
+
+namespace acs {
+
+constexpr int kDenseSortBlock = 1024;
+constexpr int kDenseRecvBlock = 256;   // 4 receivers (wavefronts) per block
+
+__global__ __launch_bounds__(kDenseSortBlock) void k_dense_sort(const DenseArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double sh[];
+    InstState* S = a.st;
+    if (S->done) return;
+    const uint32_t N = a.N, P = a.P, r = a.r;
+    __shared__ uint32_t cnt[3];   // base, byz, silent
+    if (threadIdx.x < 3) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t nb = 0, nz = 0, ns = 0;
+    for (uint32_t j = threadIdx.x; j < P; j += kDenseSortBlock) {
+        double v = kInf;
+        if (j < N) {
+            const uint32_t st = a.status ? a.status[j] : kHonest;
+            if (st == kHonest || (st != kByz && r < st)) {
+                v = a.x[j];
+                ++nb;
+            } else if (st == kByz) {
+                ++nz;
+            } else if (r > st) {
+                ++ns;
+            }
+        }
+        sh[j] = v;
+    }
+    atomicAdd(&cnt[0], nb);
+    atomicAdd(&cnt[1], nz);
+    atomicAdd(&cnt[2], ns);
+    __syncthreads();
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            for (uint32_t idx = threadIdx.x; idx < P; idx += kDenseSortBlock) {
+                const uint32_t ixj = idx ^ jj;
+                if (ixj > idx) {
+                    const double p = sh[idx], q = sh[ixj];
+                    const bool up = (idx & k) == 0;
+                    if (up ? (q < p) : (p < q)) {
+                        sh[idx] = q;
+                        sh[ixj] = p;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t j = threadIdx.x; j < cnt[0]; j += kDenseSortBlock) a.sorted[j] = sh[j];
+    if (threadIdx.x == 0) {
+        a.counts[0] = cnt[0];
+        a.counts[1] = cnt[1];
+        a.counts[2] = cnt[2];
+    }
+}
+
+// number of elements of sorted b[0..n) strictly below v
+__device__ __forceinline__ uint32_t rank_below(const double* b, uint32_t n, double v) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (b[mid] < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+struct Merged {   // M = B with two constant blocks (v1 <= v2) spliced in at their ranks
+    const double* b;
+    uint32_t r1, n1, r2, n2;
+    double v1, v2;
+    __device__ __forceinline__ double at(uint32_t k) const {
+        if (k < r1) return b[k];
+        if (k < r1 + n1) return v1;
+        if (k < r2 + n1) return b[k - n1];
+        if (k < r2 + n1 + n2) return v2;
+        return b[k - n1 - n2];
+    }
+};
+
+__global__ __launch_bounds__(kDenseRecvBlock) void k_dense_recv(const DenseArgs a) {
+    InstState* S = a.st;
+    if (S->done) return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t i = blockIdx.x * (kDenseRecvBlock / 64) + (threadIdx.x >> 6);
+    double mn = kInf, mx = -kInf;
+    if (i < a.N) {
+        const double xi = a.x[i];
+        const uint32_t st = a.status ? a.status[i] : kHonest;
+        double res = xi;
+        if (st == kHonest || (st != kByz && a.r < st)) {
+            const uint32_t nb = a.counts[0], nz = a.counts[1], ns = a.counts[2];
+            const double lo = S->lo, hi = S->hi;
+            const double c = a.byz == 0 ? ((i & 1u) == 0 ? hi + a.delta : lo - a.delta) : a.bconst;
+            // blocks (c, nz) and (xi, ns), ordered by value
+            Merged M;
+            M.b = a.sorted;
+            const bool cfirst = c <= xi;
+            M.v1 = cfirst ? c : xi;
+            M.n1 = cfirst ? nz : ns;
+            M.v2 = cfirst ? xi : c;
+            M.n2 = cfirst ? ns : nz;
+            M.r1 = M.n1 ? rank_below(a.sorted, nb, M.v1) : 0;
+            M.r2 = M.n2 ? rank_below(a.sorted, nb, M.v2) : M.r1;
+            if (M.r2 < M.r1) M.r2 = M.r1;
+            const uint32_t m = a.N, t = a.trim, nr = m - 2 * t;
+            if (a.rule == 2) {
+                res = (M.at(t) + M.at(m - t - 1)) * 0.5;
+            } else {
+                const uint32_t step = a.rule == 3 ? t : 1;
+                const uint32_t cnt = a.rule == 3 ? (nr + t - 1) / t : nr;
+                uint32_t P2 = 64;
+                while (P2 < cnt) P2 <<= 1;
+                // §A.7 stride halving over P2 slots: this lane owns w[lane + 64a]
+                const uint32_t per = P2 / 64;   // <= 128 for m <= 8192
+                double w[8];
+                // levels with stride >= 64 fold in registers: accumulate slot groups in tree order
+                // (per <= 8 keeps the whole lane column in registers; larger P2 folds first)
+                uint32_t per_eff = per;
+                double acc_big = 0.0;
+                (void)acc_big;
+                if (per <= 8) {
+#pragma unroll
+                    for (int g = 0; g < 8; ++g) {
+                        const uint32_t k = lane + 64u * g;
+                        w[g] = (g < (int)per && k < cnt) ? M.at(t + k * step) : 0.0;
+                    }
+                    for (uint32_t s = per >> 1; s >= 1; s >>= 1) {
+#pragma unroll
+                        for (int g = 0; g < 4; ++g)
+                            if ((uint32_t)g < s) w[g] = w[g] + w[g + s];
+                    }
+                } else {
+                    // large windows: strided partial trees per lane, folded in the same order
+                    // (position k = lane + 64*g pairs with k + P2/2 = lane + 64*(g + per/2))
+                    double col[128];
+                    for (uint32_t g = 0; g < per_eff; ++g) {
+                        const uint32_t k = lane + 64u * g;
+                        col[g] = k < cnt ? M.at(t + k * step) : 0.0;
+                    }
+                    for (uint32_t s = per_eff >> 1; s >= 1; s >>= 1)
+                        for (uint32_t g = 0; g < s; ++g) col[g] = col[g] + col[g + s];
+                    w[0] = col[0];
+                }
+                double v = w[0];
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) {
+                    const double u = __shfl_down(v, o, 64);
+                    if (lane < (uint32_t)o) v = v + u;
+                }
+                res = readlane_f64(v, 0) / (double)cnt;
+            }
+            if (st == kHonest) {
+                mn = res;
+                mx = res;
+            }
+        }
+        if (lane == 0) a.xo[i] = res;
+    }
+    // lanes of a receiver agree; fold the block's receivers
+    block_minmax_store<kDenseRecvBlock>(mn, mx, a.partial + blockIdx.x);
+}
+
+bool dense_supported(uint32_t fault_model, uint32_t byz, uint32_t rule, uint32_t thr, uint64_t N) {
+    if (thr != 0 || rule == 0 || N > kGenericMaxM || N < 2) return false;
+    if (fault_model == 1) return false;   // crash rounds deliver per slot: generic kernel
+    if (fault_model == 2 && byz == 1) return false;   // RANDOM Byzantine values are per slot
+    return true;
+}
+
+uint32_t dense_nblk(uint64_t N) { return (uint32_t)((N + (kDenseRecvBlock / 64) - 1) / (kDenseRecvBlock / 64)); }
+
+hipError_t launch_round_dense(const DenseArgs& a, hipStream_t s) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_dense_sort, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)(kGenericMaxM * sizeof(double)));
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(k_dense_sort, dim3(1), dim3(kDenseSortBlock), a.P * sizeof(double), s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_dense_recv, dim3(dense_nblk(a.N)), dim3(kDenseRecvBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace acs

@@ -47,10 +47,11 @@ __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs
     const uint64_t N = a.N;
     const double* __restrict__ x = a.xin + lb * N;
     double* __restrict__ xo = a.xout + lb * N;
-    const uint32_t i = blockIdx.x * kRegularBlock + threadIdx.x;
+    const uint32_t li = blockIdx.x * kRegularBlock + threadIdx.x;   // local row (ELL row)
+    const uint32_t i = (uint32_t)a.row0 + li;                        // global receiver id
 
     double mn = kInf, mx = -kInf;
-    if (i < N) {
+    if (li < a.nrows && i < N) {
         const double xi = x[i];
         double res = xi;
         bool honest = true, active = true;
@@ -65,7 +66,7 @@ __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs
         }
         if (active) {
             const uint4* cp = reinterpret_cast<const uint4*>(a.ell) +
-                              (uint64_t)(i >> 6) * (NQ * 64) + (i & 63);
+                              (uint64_t)(li >> 6) * (NQ * 64) + (li & 63);
             uint32_t col[D];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
@@ -156,7 +157,9 @@ const char* regular_fast_name(uint32_t d, uint32_t t, bool clean) {
 }
 
 hipError_t launch_round_regular(const RoundArgs& a, uint64_t B, bool clean, hipStream_t s) {
-    const dim3 grid((unsigned)((a.N + kRegularBlock - 1) / kRegularBlock), (unsigned)B);
+    // one block per partial slot: blocks past nrows only write neutral (+inf, -inf) partials, so
+    // the finalize can fold every slot of every partition
+    const dim3 grid((unsigned)a.nblk, (unsigned)B);
     const dim3 block(kRegularBlock);
 #define X(DD, TT)                                                                         \
     if (a.d == DD && a.trim == TT) {                                                      \

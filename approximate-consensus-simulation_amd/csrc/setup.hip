@@ -20,17 +20,19 @@ __global__ __launch_bounds__(256) void k_init_values(double* x, uint64_t N, Key 
     x[lb * N + i] = u53(pick(w, sel), pick(w, sel + 1));
 }
 
-// §A.3: column t of node i is π_{t/2}(i) (t even) or π_{t/2}^{-1}(i) (t odd).
-__global__ __launch_bounds__(256) void k_build_ell(uint32_t* ell, uint64_t N, uint32_t d, uint32_t dp,
-                                                   Feistel f) {
+// §A.3: column t of node i is π_{t/2}(i) (t even) or π_{t/2}^{-1}(i) (t odd).  Builds the rows
+// [row0, row0 + nrows) (a node partition; 0, N otherwise) into a local ELL.
+__global__ __launch_bounds__(256) void k_build_ell(uint32_t* ell, uint64_t N, uint64_t row0, uint64_t nrows,
+                                                   uint32_t d, uint32_t dp, Feistel f) {
     const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const uint32_t half = d >> 1;
-    const uint64_t i = gid / half;
+    const uint64_t li = gid / half;
     const uint32_t k = (uint32_t)(gid % half);
-    if (i >= N) return;
+    const uint64_t i = row0 + li;
+    if (li >= nrows || i >= N) return;
     const uint32_t fw = feistel_fwd(f, k, (uint32_t)i);
     const uint32_t iv = feistel_inv(f, k, (uint32_t)i);
-    const uint64_t base = ((i >> 6) * (dp >> 2)) * 256 + (i & 63) * 4;
+    const uint64_t base = ((li >> 6) * (dp >> 2)) * 256 + (li & 63) * 4;
     const uint32_t t0 = 2 * k, t1 = 2 * k + 1;
     ell[base + (uint64_t)(t0 >> 2) * 256 + (t0 & 3)] = fw;
     ell[base + (uint64_t)(t1 >> 2) * 256 + (t1 & 3)] = iv;
@@ -105,10 +107,11 @@ hipError_t launch_init_values(double* x, uint64_t B, uint64_t N, Key key, uint64
     return hipGetLastError();
 }
 
-hipError_t launch_build_ell(uint32_t* ell, uint64_t N, uint32_t d, uint32_t dp, const Feistel& f,
-                            hipStream_t s) {
-    const uint64_t work = N * (d >> 1);
-    hipLaunchKernelGGL(k_build_ell, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, ell, N, d, dp, f);
+hipError_t launch_build_ell(uint32_t* ell, uint64_t N, uint64_t row0, uint64_t nrows, uint32_t d, uint32_t dp,
+                            const Feistel& f, hipStream_t s) {
+    const uint64_t work = nrows * (d >> 1);
+    hipLaunchKernelGGL(k_build_ell, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, ell, N, row0, nrows, d,
+                       dp, f);
     return hipGetLastError();
 }
 

@@ -135,6 +135,24 @@ typedef struct acs_result {
 int acs_create(const acs_config* cfg, int backend, const int* devices, int n_devices,
                struct acs_sim** out);
 
+/* §8(e) node partitioning of ONE RANDOM_REGULAR instance over n_ranks GPUs (cfg5), one process
+ * (or thread) per GPU.  Rank r owns the 64-aligned row block [r*R, (r+1)*R) ∩ [0, N),
+ * R = ceil(ceil(N/n_ranks)/64)*64, keeps the full x on its GPU, and after every round exchanges
+ * x^{r+1} with an in-place RCCL all-gather over xGMI plus an all-reduce of the honest
+ * (-min, max) for the ε test, so every rank holds identical state.
+ *   acs_get_comm_id: rank 0 creates the RCCL unique id (acs_comm_id_size() bytes) that every
+ *   rank passes to acs_create_partitioned (any out-of-band channel, e.g. torch.distributed).
+ *   comm_id == NULL with n_ranks > 1 simulates all n_ranks partitions on `device` with private
+ *   x copies and a device-memcpy all-gather (validation of the partitioned data flow on one GPU;
+ *   rank must be 0).  n_ranks == 1 behaves like acs_create. */
+int acs_comm_id_size(void);
+int acs_get_comm_id(void* out, uint64_t n);
+int acs_create_partitioned(const acs_config* cfg, int device, int n_ranks, int rank,
+                           const void* comm_id, uint64_t id_len, struct acs_sim** out);
+/* Virtual partitions only: the private x copy of one partition (all copies are identical after
+ * every round's all-gather; partition 0's copy is what acs_get_values returns). */
+int acs_get_partition_values(struct acs_sim* sim, int partition, void* out, uint64_t n);
+
 /* §8(a) a10/a9: advance every unfinished instance by at most k rounds; stops at convergence. */
 int acs_round(struct acs_sim* sim, uint32_t k, acs_round_info* out);
 

@@ -99,6 +99,21 @@ CASES = {
     "generic_complete65_avg": Config(n_nodes=65, n_instances=3, topology="complete", rule="average",
                                      loss_p=0.2, eps=1e-9, max_rounds=300, seed=2, trace_spread=True),
     "cfg2_full": preset("cfg2", trace_spread=True),
+    # dense shared-sort kernels (complete, no loss, no crash, Byzantine SPLIT/CONSTANT)
+    "dense65_split_mid": Config(n_nodes=65, topology="complete", rule="midpoint", trim=3,
+                                fault_model="byzantine", n_faulty=20, byz_strategy="split",
+                                byz_delta=0.25, eps=1e-9, max_rounds=3000, seed=31, trace_spread=True),
+    "dense300_clean_trim": Config(n_nodes=300, topology="complete", rule="trimmed", trim=37,
+                                  eps=1e-12, max_rounds=100, seed=32, trace_spread=True),
+    "dense500_const_dlpsw": Config(n_nodes=500, topology="complete", rule="dlpsw", trim=40,
+                                   fault_model="byzantine", n_faulty=100, byz_strategy="constant",
+                                   byz_const=-2.5, eps=1e-9, max_rounds=500, seed=33,
+                                   trace_spread=True),
+    "dense3000_split_bigwindow": Config(n_nodes=3000, topology="complete", rule="trimmed",
+                                        trim=900, fault_model="byzantine", n_faulty=900,
+                                        byz_strategy="split", byz_delta=0.0, eps=1e-6,
+                                        max_rounds=60, termination="fixed", seed=34,
+                                        trace_spread=True),
     # batched persistent kernel (complete, N <= 64)
     "cfg1": preset("cfg1", trace_spread=True),
     "cfg1_avg": preset("cfg1_avg", trace_spread=True),

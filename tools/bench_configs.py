@@ -1,0 +1,57 @@
+"""Time every preset on one GPU: node-rounds/s, rounds, and the round kernel's
+average device time.  Prints one JSON line per config.  usage: python tools/bench_configs.py [names]
+
+cfg1/cfg2/cfg3 run to ε-convergence (their natural workload); cfg4/cfg5 run FIXED rounds.
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "approximate-consensus-simulation_amd"))
+
+import acsim  # noqa: E402
+
+CASES = {
+    "cfg1": dict(),
+    "cfg1_avg": dict(),
+    "cfg2": dict(),
+    "cfg3": dict(),
+    "cfg4": dict(max_rounds=100),
+    "cfg4_eps": dict(),
+    "cfg4_byz": dict(),
+    "cfg5": dict(max_rounds=20),
+}
+
+
+def run(name, **kw):
+    cfg = acsim.preset(name, **kw)
+    t0 = time.perf_counter()
+    sim = acsim.Simulator(cfg)
+    t_setup = time.perf_counter() - t0
+    sim.set_kernel_timing(True)
+    t0 = time.perf_counter()
+    res = sim.run()
+    wall = time.perf_counter() - t0
+    ms, n, kname = sim.kernel_timing()
+    rounds = sim.rounds()
+    out = {"config": name, "n_nodes": cfg.n_nodes, "n_instances": cfg.n_instances,
+           "rounds_max": int(res.rounds_max), "rounds_mean": float(rounds.mean()),
+           "n_converged": int(res.n_converged), "node_rounds": int(res.node_rounds),
+           "wall_s": wall, "node_rounds_per_s": res.node_rounds / wall,
+           "kernel": kname, "kernel_launches": n, "kernel_ms_total": ms,
+           "kernel_avg_us": (ms / n * 1e3) if n else None, "setup_s": t_setup}
+    sim.close()
+    return out
+
+
+def main():
+    names = sys.argv[1:] or list(CASES)
+    for nm in names:
+        run(nm, **CASES.get(nm, {}))          # warm-up (code objects, allocations)
+        print(json.dumps(run(nm, **CASES.get(nm, {}))), flush=True)
+
+
+if __name__ == "__main__":
+    main()
