@@ -510,7 +510,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
 
     if (cfg->topology == ACS_TOPO_COMPLETE && s->N <= kBatchedMaxN) {
         s->path = PATH_BATCHED;
-        s->kname = batched_small_name((uint32_t)s->N, cfg->rule);
+        s->kname = batched_small_name((uint32_t)s->N, cfg->rule, cfg->fault_model != ACS_FAULT_NONE);
     } else if (cfg->topology == ACS_TOPO_COMPLETE && s->B == 1 && !partitioned &&
                dense_supported(cfg->fault_model, cfg->byz_strategy, cfg->rule, s->mp.thr, s->N)) {
         s->path = PATH_DENSE;

@@ -12,6 +12,8 @@
 //     runtime-t window read back from a lane-private LDS column;
 //   - honest (min, max) by wavefront shuffles, ε test, early exit per instance (§A.8).
 // HBM traffic: 8N bytes in and out per instance per launch.  Bound: integer VALU (Philox).
+#include <stdio.h>
+
 #include "resolve.hpp"
 #include "sortnet.hpp"
 
@@ -65,25 +67,36 @@ struct LaneCtx {
     uint64_t miss;   // bit j: message from j missing (crash or drop)
 };
 
-// §A.6 entry j of receiver `lane` (valid for j < N)
+// Byzantine value kept out of line: inlined into each of the P unrolled leaves it multiplied the
+// code (one Philox call per leaf) and spilled registers.
+__device__ __noinline__ double byz_value_ool(const MsgParams& mp, uint32_t b, uint32_t r, uint32_t i, uint64_t s,
+                                             double lo, double hi) {
+    return byz_value(mp, b, r, i, s, lo, hi);
+}
+
+// §A.6 entry j of receiver `lane` (valid for j < N).  FAULTS = false: no fault schedule, so a
+// sender is never Byzantine and only the drop bits matter (cfg3).
+template <bool FAULTS>
 __device__ __forceinline__ double entry_value(const LaneCtx& c, int j) {
     const double xj = readlane_f64(c.xi, j);
-    const uint32_t stj = (uint32_t)__builtin_amdgcn_readlane((int)c.sti, j);
     if ((uint32_t)j == c.lane) return c.xi;
     if ((c.miss >> j) & 1ull) return c.xi;
-    if (stj == kByz) return byz_value(*c.mp, c.b, c.r, c.lane, (uint64_t)c.lane * c.N + j, c.lo, c.hi);
+    if constexpr (FAULTS) {
+        const uint32_t stj = (uint32_t)__builtin_amdgcn_readlane((int)c.sti, j);
+        if (stj == kByz) return byz_value_ool(*c.mp, c.b, c.r, c.lane, (uint64_t)c.lane * c.N + j, c.lo, c.hi);
+    }
     return xj;
 }
 
-template <int P, int... Q>
+template <int P, bool FAULTS, int... Q>
 __device__ __forceinline__ double average_tree(const LaneCtx& c, std::integer_sequence<int, Q...>) {
     constexpr int LOG2P = ilog2(P);
     double acc[LOG2P + 1];
-    (push_leaf<P, Q, LOG2P>(acc, (bitrev<LOG2P>(Q) < (int)c.N) ? entry_value(c, bitrev<LOG2P>(Q)) : 0.0), ...);
+    (push_leaf<P, Q, LOG2P>(acc, (bitrev<LOG2P>(Q) < (int)c.N) ? entry_value<FAULTS>(c, bitrev<LOG2P>(Q)) : 0.0), ...);
     return acc[LOG2P];
 }
 
-template <int P, bool SORT>
+template <int P, bool SORT, bool FAULTS>
 __global__ __launch_bounds__(64) void k_batched_small(const BatchArgs a, uint32_t kmax) {
     const uint32_t lb = blockIdx.x;
     const uint32_t lane = threadIdx.x;
@@ -124,7 +137,7 @@ __global__ __launch_bounds__(64) void k_batched_small(const BatchArgs a, uint32_
             }
         }
         // crash bits (§A.4): sender status is uniform per j
-        if (mp.fault == 1 && act) {
+        if (FAULTS && mp.fault == 1 && act) {
             for (uint32_t j = 0; j < N; ++j) {
                 const uint32_t stj = (uint32_t)__builtin_amdgcn_readlane((int)sti, (int)j);
                 if (stj < kByz && r >= stj && crash_missing(mp, stj, b, r, (uint64_t)lane * N + j))
@@ -133,11 +146,11 @@ __global__ __launch_bounds__(64) void k_batched_small(const BatchArgs a, uint32_
         }
         double res;
         if constexpr (!SORT) {
-            res = average_tree<P>(c, std::make_integer_sequence<int, P>{}) / (double)N;
+            res = average_tree<P, FAULTS>(c, std::make_integer_sequence<int, P>{}) / (double)N;
         } else {
             double v[P];
 #pragma unroll
-            for (int j = 0; j < P; ++j) v[j] = j < (int)N ? entry_value(c, j) : kInf;
+            for (int j = 0; j < P; ++j) v[j] = j < (int)N ? entry_value<FAULTS>(c, j) : kInf;
             select_sort<P>(v);
 #pragma unroll
             for (int k = 0; k < P; ++k) colbuf[k * 64 + lane] = v[k];
@@ -186,24 +199,25 @@ static int pick_p(uint32_t N) {
     return P;
 }
 
-const char* batched_small_name(uint32_t N, uint32_t rule) {
-    static const char* names[2][6] = {
-        {"k_batched_small<2,avg>", "k_batched_small<4,avg>", "k_batched_small<8,avg>",
-         "k_batched_small<16,avg>", "k_batched_small<32,avg>", "k_batched_small<64,avg>"},
-        {"k_batched_small<2,sort>", "k_batched_small<4,sort>", "k_batched_small<8,sort>",
-         "k_batched_small<16,sort>", "k_batched_small<32,sort>", "k_batched_small<64,sort>"}};
-    return names[rule != 0][ilog2(pick_p(N)) - 1];
+const char* batched_small_name(uint32_t N, uint32_t rule, bool faults) {
+    static char names[2][2][7][40];
+    const int P = pick_p(N), lp = ilog2(P), so = rule != 0, fa = faults ? 1 : 0;
+    char* nm = names[so][fa][lp];
+    if (!nm[0]) snprintf(nm, 40, "k_batched_small<%d,%s,%s>", P, so ? "sort" : "avg", fa ? "faulty" : "clean");
+    return nm;
 }
 
 hipError_t launch_batched_small(const BatchArgs& a, uint64_t B, uint32_t k, hipStream_t s) {
     if (a.N < 1 || a.N > kBatchedMaxN) return hipErrorNotSupported;
     const int P = pick_p(a.N);
-    const bool sort = a.rule != 0;
+    const bool sort = a.rule != 0, faults = a.status != nullptr;
     const dim3 grid((unsigned)B), block(64);
-#define L(PP)                                                                              \
-    case PP:                                                                               \
-        if (sort) hipLaunchKernelGGL((k_batched_small<PP, true>), grid, block, 0, s, a, k);  \
-        else hipLaunchKernelGGL((k_batched_small<PP, false>), grid, block, 0, s, a, k);     \
+#define L(PP)                                                                                        \
+    case PP:                                                                                         \
+        if (sort && faults) hipLaunchKernelGGL((k_batched_small<PP, true, true>), grid, block, 0, s, a, k);   \
+        else if (sort) hipLaunchKernelGGL((k_batched_small<PP, true, false>), grid, block, 0, s, a, k);       \
+        else if (faults) hipLaunchKernelGGL((k_batched_small<PP, false, true>), grid, block, 0, s, a, k);     \
+        else hipLaunchKernelGGL((k_batched_small<PP, false, false>), grid, block, 0, s, a, k);                \
         break;
     switch (P) {
         L(2) L(4) L(8) L(16) L(32) L(64)

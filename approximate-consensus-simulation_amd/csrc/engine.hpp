@@ -123,6 +123,6 @@ hipError_t launch_round_dense(const DenseArgs& a, hipStream_t s);
 // state in VGPRs across rounds.
 constexpr uint32_t kBatchedMaxN = 64;
 hipError_t launch_batched_small(const BatchArgs& a, uint64_t B, uint32_t k, hipStream_t s);
-const char* batched_small_name(uint32_t N, uint32_t rule);
+const char* batched_small_name(uint32_t N, uint32_t rule, bool faults);
 
 }  // namespace acs
