@@ -19,7 +19,7 @@ STATUS_NAMES = {OK: "OK", EINVAL: "EINVAL", ENOMEM: "ENOMEM", EDEVICE: "EDEVICE"
 BACKEND_CPU, BACKEND_HIP = 0, 1
 
 # topology / rule / faults / byz / termination / dtype
-TOPO_COMPLETE, TOPO_RANDOM_REGULAR = 0, 1
+TOPO_COMPLETE, TOPO_RANDOM_REGULAR, TOPO_CSR = 0, 1, 2
 RULE_AVERAGE, RULE_TRIMMED_MEAN, RULE_MIDPOINT, RULE_DLPSW_SELECT = 0, 1, 2, 3
 FAULT_NONE, FAULT_CRASH, FAULT_BYZANTINE = 0, 1, 2
 BYZ_SPLIT, BYZ_RANDOM, BYZ_CONSTANT = 0, 1, 2
@@ -103,6 +103,7 @@ def _declare(lib: C.CDLL) -> None:
     P = C.POINTER
     sigs = {
         "acs_create": (i32, [P(AcsConfig), i32, P(C.c_int), i32, P(vp)]),
+        "acs_create_csr": (i32, [P(AcsConfig), P(u64), P(u32), i32, P(vp)]),
         "acs_comm_id_size": (i32, []),
         "acs_get_comm_id": (i32, [vp, u64]),
         "acs_create_partitioned": (i32, [P(AcsConfig), i32, i32, i32, vp, u64, P(vp)]),

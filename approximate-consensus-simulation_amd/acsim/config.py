@@ -13,7 +13,7 @@ from . import _abi
 
 _ENUMS = {
     "topology": {"complete": _abi.TOPO_COMPLETE, "random_regular": _abi.TOPO_RANDOM_REGULAR,
-                 "regular": _abi.TOPO_RANDOM_REGULAR},
+                 "regular": _abi.TOPO_RANDOM_REGULAR, "csr": _abi.TOPO_CSR},
     "rule": {"average": _abi.RULE_AVERAGE, "trimmed_mean": _abi.RULE_TRIMMED_MEAN,
              "trimmed": _abi.RULE_TRIMMED_MEAN, "midpoint": _abi.RULE_MIDPOINT,
              "dlpsw": _abi.RULE_DLPSW_SELECT, "dlpsw_select": _abi.RULE_DLPSW_SELECT},

@@ -43,7 +43,8 @@ class Simulator:
     """One device-resident simulation handle (``acs_sim``)."""
 
     def __init__(self, cfg: Config | str, device: int = 0, backend: str = "hip",
-                 partitions: int = 1, rank: int = 0, comm_id: Optional[bytes] = None):
+                 partitions: int = 1, rank: int = 0, comm_id: Optional[bytes] = None,
+                 csr=None):
         """partitions > 1 node-partitions one RANDOM_REGULAR instance: with
         comm_id (RCCL unique id from acsim.distributed) this handle is `rank`'s partition on
         `device`; without it all partitions are simulated on `device` with private x copies
@@ -58,7 +59,14 @@ class Simulator:
         self._lib = _abi.load_library()
         self._c = cfg.to_c()
         h = C.c_void_p()
-        if self.partitions == 1 and comm_id is None:
+        if csr is not None:   # user graph (topology="csr"): csr = (rowptr[N+1], colidx[nnz])
+            rp = np.ascontiguousarray(csr[0], dtype=np.uint64)
+            ci = np.ascontiguousarray(csr[1], dtype=np.uint32)
+            if rp.size != int(cfg.n_nodes) + 1:
+                raise ValueError("rowptr must have n_nodes + 1 entries")
+            rc = self._lib.acs_create_csr(C.byref(self._c), rp.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                          ci.ctypes.data_as(C.POINTER(C.c_uint32)), int(device), C.byref(h))
+        elif self.partitions == 1 and comm_id is None:
             devs = (C.c_int * 1)(int(device))
             rc = self._lib.acs_create(C.byref(self._c), _abi.BACKEND_HIP, devs, 1, C.byref(h))
         else:
@@ -186,7 +194,8 @@ class Simulator:
 
 
 def simulate(cfg: Config | str, backend: str = "hip", device: int = 0,
-             devices: Optional[Sequence[int]] = None, return_values: bool = True) -> Result:
+             devices: Optional[Sequence[int]] = None, return_values: bool = True,
+             csr=None) -> Result:
     """Run one configuration to termination and return its results."""
     if devices is not None:
         devices = list(devices)
@@ -194,7 +203,7 @@ def simulate(cfg: Config | str, backend: str = "hip", device: int = 0,
             raise ValueError("simulate() drives one device per process; shard instances across "
                              "processes with acsim.distributed (one rank per GPU)")
         device = devices[0]
-    with Simulator(cfg, device=device, backend=backend) as sim:
+    with Simulator(cfg, device=device, backend=backend, csr=csr) as sim:
         res = sim.run()
         x = None
         if return_values:

@@ -80,6 +80,8 @@ struct acs_sim {
     uint64_t rows_per = 0, Npad = 0;
     ncclComm_t comm = nullptr;
     double2* gpart = nullptr;      // (-min, max) exchanged by all-reduce
+    uint64_t* rowptr = nullptr;    // CSR topology (device copies)
+    uint32_t* colidx = nullptr;
     double* dsorted = nullptr;     // dense path: sorted base multiset [N]
     uint32_t* dcounts = nullptr;   // dense path: |B|, #Byzantine, #crash-silent
     std::vector<Part> parts;       // virtual partitions 1..P-1 (partition 0 uses x / ell)
@@ -111,10 +113,18 @@ static int validate(const acs_config* c) {
             return fail(ACS_EINVAL, "degree must be even, in [2, 4096]");
         m = (uint64_t)c->degree + 1;
         slots = c->n_nodes * (uint64_t)c->degree;
+    } else if (c->topology == ACS_TOPO_CSR) {
+        m = 0;       // per receiver: checked against the arrays in acs_create_csr
+        slots = 0;
     } else {
         return fail(ACS_EINVAL, "unknown topology %u", c->topology);
     }
     if (slots >= (1ull << 34)) return fail(ACS_EINVAL, "slot count must be < 2^34");
+    if (c->topology == ACS_TOPO_CSR) {
+        if (c->rule > ACS_RULE_DLPSW_SELECT) return fail(ACS_EINVAL, "unknown rule %u", c->rule);
+        if (c->rule == ACS_RULE_AVERAGE && c->trim != 0) return fail(ACS_EINVAL, "AVERAGE requires trim == 0");
+        if (c->rule == ACS_RULE_DLPSW_SELECT && c->trim < 1) return fail(ACS_EINVAL, "DLPSW needs t >= 1");
+    } else
     switch (c->rule) {
         case ACS_RULE_AVERAGE:
             if (c->trim != 0) return fail(ACS_EINVAL, "AVERAGE requires trim == 0");
@@ -181,6 +191,8 @@ static void release(acs_sim* s) {
     (void)hipFree(s->st);
     (void)hipFree(s->partial);
     (void)hipFree(s->gpart);
+    (void)hipFree(s->rowptr);
+    (void)hipFree(s->colidx);
     (void)hipFree(s->dsorted);
     (void)hipFree(s->dcounts);
     (void)hipFree(s->n_done);
@@ -275,6 +287,8 @@ static RoundArgs round_args(acs_sim* s, uint32_t r) {
     a.N = s->N;
     a.row0 = 0;
     a.nrows = s->N;
+    a.rowptr = s->rowptr;
+    a.colidx = s->colidx;
     a.m = (uint32_t)s->m;
     a.d = s->d;
     a.dp = s->dp;
@@ -463,11 +477,34 @@ static hipError_t build_rows(acs_sim* s, uint32_t* ell, int p) {
 }
 
 static int create_impl(const acs_config* cfg, int device, int nranks, int rank, const void* comm_id,
-                       uint64_t id_len, acs_sim** out) {
+                       uint64_t id_len, acs_sim** out, const uint64_t* h_rowptr = nullptr,
+                       const uint32_t* h_colidx = nullptr) {
     if (!out) return fail(ACS_EINVAL, "null out");
     *out = nullptr;
     int rc = validate(cfg);
     if (rc) return rc;
+    uint64_t csr_mmax = 0, csr_nnz = 0;
+    if (cfg->topology == ACS_TOPO_CSR) {   // §8(f) row 1: check the arrays on the host
+        if (!h_rowptr || !h_colidx) return fail(ACS_EINVAL, "CSR topology needs acs_create_csr(rowptr, colidx)");
+        if (nranks != 1) return fail(ACS_EUNSUPPORTED, "node partitioning needs RANDOM_REGULAR");
+        const uint64_t N = cfg->n_nodes;
+        if (h_rowptr[0] != 0) return fail(ACS_EINVAL, "rowptr[0] must be 0");
+        csr_mmax = 1;
+        for (uint64_t i = 0; i < N; ++i) {
+            if (h_rowptr[i + 1] < h_rowptr[i]) return fail(ACS_EINVAL, "rowptr must be non-decreasing");
+            const uint64_t m = h_rowptr[i + 1] - h_rowptr[i] + 1;
+            if (cfg->rule != ACS_RULE_AVERAGE && m <= 2ull * cfg->trim)
+                return fail(ACS_EINVAL, "receiver %llu has m = %llu <= 2t", (unsigned long long)i,
+                            (unsigned long long)m);
+            if (m > csr_mmax) csr_mmax = m;
+        }
+        csr_nnz = h_rowptr[N];
+        if (csr_nnz >= (1ull << 34)) return fail(ACS_EINVAL, "slot count must be < 2^34");
+        if (cfg->fault_model == ACS_FAULT_BYZANTINE && cfg->byz_strategy == ACS_BYZ_RANDOM && csr_nnz > (1ull << 33))
+            return fail(ACS_EINVAL, "BYZ RANDOM needs slot count <= 2^33");
+        for (uint64_t k = 0; k < csr_nnz; ++k)
+            if (h_colidx[k] >= N) return fail(ACS_EINVAL, "colidx[%llu] out of range", (unsigned long long)k);
+    }
     if (nranks < 1 || rank < 0 || rank >= nranks) return fail(ACS_EINVAL, "bad rank / n_ranks");
     const bool partitioned = nranks > 1 || comm_id != nullptr;
     const bool virt = partitioned && !comm_id;
@@ -489,8 +526,10 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     s->device = device;
     s->N = cfg->n_nodes;
     s->B = cfg->n_instances;
-    s->m = cfg->topology == ACS_TOPO_COMPLETE ? s->N : (uint64_t)cfg->degree + 1;
-    s->d = cfg->degree;
+    s->m = cfg->topology == ACS_TOPO_COMPLETE ? s->N
+         : cfg->topology == ACS_TOPO_CSR      ? csr_mmax
+                                              : (uint64_t)cfg->degree + 1;
+    s->d = cfg->topology == ACS_TOPO_CSR ? 0 : cfg->degree;
     s->dp = (cfg->degree + 3u) & ~3u;
     s->clean = cfg->fault_model == ACS_FAULT_NONE && drop_threshold(cfg->loss_p) == 0;
     s->mp.key = key_of(cfg->seed);
@@ -596,6 +635,12 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         CREATE_TRY(build_fault_status(s->status, s->B, s->N, cfg->n_faulty, cfg->fault_model,
                                       cfg->crash_window, s->mp.key, cfg->instance_offset, s->stream));
     }
+    if (cfg->topology == ACS_TOPO_CSR) {
+        CREATE_TRY(hipMalloc(&s->rowptr, (s->N + 1) * sizeof(uint64_t)));
+        CREATE_TRY(hipMalloc(&s->colidx, (csr_nnz ? csr_nnz : 1) * sizeof(uint32_t)));
+        CREATE_TRY(hipMemcpy(s->rowptr, h_rowptr, (s->N + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
+        if (csr_nnz) CREATE_TRY(hipMemcpy(s->colidx, h_colidx, csr_nnz * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
     CREATE_TRY(launch_init_values(s->x[0], s->B, s->N, s->mp.key, cfg->instance_offset, s->stream));
     for (Part& q : s->parts) CREATE_TRY(launch_init_values(q.x[0], s->B, s->N, s->mp.key, cfg->instance_offset, s->stream));
 #undef CREATE_TRY
@@ -634,7 +679,16 @@ int acs_create(const acs_config* cfg, int backend, const int* devices, int n_dev
                                       "test oracle in oracle/, not a product backend)");
     if (n_devices != 1 || !devices)
         return fail(ACS_EINVAL, "exactly one device per handle (shard across processes, one rank per GPU)");
+    if (cfg->topology == ACS_TOPO_CSR) return fail(ACS_EINVAL, "CSR topology: use acs_create_csr");
     return create_impl(cfg, devices[0], 1, 0, nullptr, 0, out);
+}
+
+int acs_create_csr(const acs_config* cfg, const uint64_t* rowptr, const uint32_t* colidx, int device,
+                   acs_sim** out) {
+    if (out) *out = nullptr;
+    if (!cfg || cfg->topology != ACS_TOPO_CSR) return fail(ACS_EINVAL, "config topology must be ACS_TOPO_CSR");
+    if (!rowptr || !colidx) return fail(ACS_EINVAL, "null CSR arrays");
+    return create_impl(cfg, device, 1, 0, nullptr, 0, out, rowptr, colidx);
 }
 
 int acs_comm_id_size(void) { return (int)sizeof(ncclUniqueId); }

@@ -37,6 +37,8 @@ struct RoundArgs {
     double2* partial;         // [B][nblk]
     uint64_t N;
     uint64_t row0, nrows;     // receivers handled by this launch (node partition; 0, N otherwise)
+    const uint64_t* rowptr;   // CSR topology: [N+1] row offsets (slot of entry 1+t = rowptr[i]+t)
+    const uint32_t* colidx;   // CSR topology: [rowptr[N]] sender ids
     uint32_t m;               // entries per receiver
     uint32_t d, dp;           // degree, degree rounded up to 4
     uint32_t topology, rule, trim;

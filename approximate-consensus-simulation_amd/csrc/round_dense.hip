@@ -45,27 +45,83 @@ __global__ __launch_bounds__(kDenseSortBlock) void k_dense_sort(const DenseArgs 
         }
         sh[j] = v;
     }
-    atomicAdd(&cnt[0], nb);
-    atomicAdd(&cnt[1], nz);
-    atomicAdd(&cnt[2], ns);
+    // wavefront sums first: 1024 LDS atomics on one address serialise
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        nb += __shfl_xor(nb, o, 64);
+        nz += __shfl_xor(nz, o, 64);
+        ns += __shfl_xor(ns, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&cnt[0], nb);
+        atomicAdd(&cnt[1], nz);
+        atomicAdd(&cnt[2], ns);
+    }
+    __syncthreads();
+    // Bitonic network over P wires held in registers: thread t owns wires t + 1024e (e < E).
+    // Compare distance j < 64: partner in the same wavefront (shuffle, no barrier);
+    // 64 <= j < 1024: partner in another wavefront (LDS exchange, one barrier pair);
+    // j >= 1024: partner in the same thread (register swap).  55 stages at P = 1024, of which
+    // only 10 touch LDS.
+    constexpr int EMAX = kGenericMaxM / kDenseSortBlock;   // 8
+    const uint32_t E = (P + kDenseSortBlock - 1) / kDenseSortBlock;
+    const uint32_t tid = threadIdx.x;
+    double v[EMAX];
+#pragma unroll
+    for (int e = 0; e < EMAX; ++e) {
+        const uint32_t idx = tid + kDenseSortBlock * e;
+        v[e] = ((uint32_t)e < E && idx < P) ? sh[idx] : kInf;
+    }
     __syncthreads();
     for (uint32_t k = 2; k <= P; k <<= 1) {
-        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-            for (uint32_t idx = threadIdx.x; idx < P; idx += kDenseSortBlock) {
-                const uint32_t ixj = idx ^ jj;
-                if (ixj > idx) {
-                    const double p = sh[idx], q = sh[ixj];
-                    const bool up = (idx & k) == 0;
-                    if (up ? (q < p) : (p < q)) {
-                        sh[idx] = q;
-                        sh[ixj] = p;
-                    }
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            if (j < 64) {
+#pragma unroll
+                for (int e = 0; e < EMAX; ++e) {
+                    if ((uint32_t)e >= E) break;
+                    const uint32_t idx = tid + kDenseSortBlock * e;
+                    const double p = __shfl_xor(v[e], (int)j, 64);
+                    const bool keep_min = ((idx & j) == 0) == ((idx & k) == 0);
+                    v[e] = keep_min ? __builtin_fmin(v[e], p) : __builtin_fmax(v[e], p);
                 }
+            } else if (j < (uint32_t)kDenseSortBlock) {
+#pragma unroll
+                for (int e = 0; e < EMAX; ++e)
+                    if ((uint32_t)e < E) sh[tid + kDenseSortBlock * e] = v[e];
+                __syncthreads();
+#pragma unroll
+                for (int e = 0; e < EMAX; ++e) {
+                    if ((uint32_t)e >= E) break;
+                    const uint32_t idx = tid + kDenseSortBlock * e;
+                    const double p = sh[idx ^ j];
+                    const bool keep_min = ((idx & j) == 0) == ((idx & k) == 0);
+                    v[e] = keep_min ? __builtin_fmin(v[e], p) : __builtin_fmax(v[e], p);
+                }
+                __syncthreads();
+            } else {
+                const uint32_t ej = j / kDenseSortBlock;   // 1, 2 or 4: partner element e ^ ej
+#define ACS_SWAP_STAGE(EJ)                                                                      \
+    _Pragma("unroll") for (int e = 0; e < EMAX; ++e) {                                          \
+        if ((e ^ EJ) > e && (uint32_t)(e ^ EJ) < E) {                                           \
+            const uint32_t idx = tid + kDenseSortBlock * e;                                     \
+            const double lo_ = __builtin_fmin(v[e], v[e ^ EJ]), hi_ = __builtin_fmax(v[e], v[e ^ EJ]); \
+            const bool asc = (idx & k) == 0;                                                    \
+            v[e] = asc ? lo_ : hi_;                                                             \
+            v[e ^ EJ] = asc ? hi_ : lo_;                                                        \
+        }                                                                                       \
+    }
+                if (ej == 1) { ACS_SWAP_STAGE(1) }
+                else if (ej == 2) { ACS_SWAP_STAGE(2) }
+                else { ACS_SWAP_STAGE(4) }
+#undef ACS_SWAP_STAGE
             }
-            __syncthreads();
         }
     }
-    for (uint32_t j = threadIdx.x; j < cnt[0]; j += kDenseSortBlock) a.sorted[j] = sh[j];
+#pragma unroll
+    for (int e = 0; e < EMAX; ++e) {
+        const uint32_t idx = tid + kDenseSortBlock * e;
+        if ((uint32_t)e < E && idx < cnt[0]) a.sorted[idx] = v[e];
+    }
     if (threadIdx.x == 0) {
         a.counts[0] = cnt[0];
         a.counts[1] = cnt[1];
@@ -98,8 +154,14 @@ struct Merged {   // M = B with two constant blocks (v1 <= v2) spliced in at the
 };
 
 __global__ __launch_bounds__(kDenseRecvBlock) void k_dense_recv(const DenseArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double shB[];   // the sorted base multiset
     InstState* S = a.st;
     if (S->done) return;
+    {
+        const uint32_t nb = a.counts[0];
+        for (uint32_t k = threadIdx.x; k < nb; k += kDenseRecvBlock) shB[k] = a.sorted[k];
+        __syncthreads();
+    }
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t i = blockIdx.x * (kDenseRecvBlock / 64) + (threadIdx.x >> 6);
     double mn = kInf, mx = -kInf;
@@ -113,14 +175,14 @@ __global__ __launch_bounds__(kDenseRecvBlock) void k_dense_recv(const DenseArgs 
             const double c = a.byz == 0 ? ((i & 1u) == 0 ? hi + a.delta : lo - a.delta) : a.bconst;
             // blocks (c, nz) and (xi, ns), ordered by value
             Merged M;
-            M.b = a.sorted;
+            M.b = shB;
             const bool cfirst = c <= xi;
             M.v1 = cfirst ? c : xi;
             M.n1 = cfirst ? nz : ns;
             M.v2 = cfirst ? xi : c;
             M.n2 = cfirst ? ns : nz;
-            M.r1 = M.n1 ? rank_below(a.sorted, nb, M.v1) : 0;
-            M.r2 = M.n2 ? rank_below(a.sorted, nb, M.v2) : M.r1;
+            M.r1 = M.n1 ? rank_below(shB, nb, M.v1) : 0;
+            M.r2 = M.n2 ? rank_below(shB, nb, M.v2) : M.r1;
             if (M.r2 < M.r1) M.r2 = M.r1;
             const uint32_t m = a.N, t = a.trim, nr = m - 2 * t;
             if (a.rule == 2) {
@@ -194,13 +256,16 @@ hipError_t launch_round_dense(const DenseArgs& a, hipStream_t s) {
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute((const void*)k_dense_sort, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)(kGenericMaxM * sizeof(double)));
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)k_dense_recv, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)(kGenericMaxM * sizeof(double)));
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     hipLaunchKernelGGL(k_dense_sort, dim3(1), dim3(kDenseSortBlock), a.P * sizeof(double), s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_dense_recv, dim3(dense_nblk(a.N)), dim3(kDenseRecvBlock), 0, s, a);
+    hipLaunchKernelGGL(k_dense_recv, dim3(dense_nblk(a.N)), dim3(kDenseRecvBlock), a.N * sizeof(double), s, a);
     return hipGetLastError();
 }
 

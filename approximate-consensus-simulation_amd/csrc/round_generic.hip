@@ -61,7 +61,13 @@ __global__ __launch_bounds__(kGenericBlock) void k_round_generic(const RoundArgs
     const MsgParams& mp = a.mp;
     const uint32_t b = (uint32_t)(mp.inst_offset + lb);
     const uint32_t bG = b - b % mp.mask_group;
-    const uint32_t r = a.r, m = a.m;
+    const uint32_t r = a.r;
+    uint32_t m = a.m;
+    uint64_t rp = 0;
+    if (a.topology == 2) {   // CSR: m_i = deg(i) + 1 (a.m is the maximum, which sized P)
+        rp = a.rowptr[i];
+        m = (uint32_t)(a.rowptr[i + 1] - rp) + 1;
+    }
     const double lo = S->lo, hi = S->hi;
     const bool avg = a.rule == 0;
     for (uint32_t e = threadIdx.x; e < P; e += kGenericBlock) {
@@ -76,6 +82,10 @@ __global__ __launch_bounds__(kGenericBlock) void k_round_generic(const RoundArgs
                 j = e;
                 slot = (uint64_t)i * N + j;
                 self = j == i;
+            } else if (a.topology == 2) {   // CSR: entry 0 self, entry 1+t from colidx[rp+t]
+                self = e == 0;
+                j = self ? i : a.colidx[rp + e - 1];
+                slot = rp + e - 1;
             } else {                 // RANDOM_REGULAR: entry 0 self, entry 1+t from nbr(i,t)
                 self = e == 0;
                 const uint32_t t = e - 1;

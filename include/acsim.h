@@ -44,6 +44,7 @@ extern "C" {
 /* topology (§A.3) */
 #define ACS_TOPO_COMPLETE        0
 #define ACS_TOPO_RANDOM_REGULAR  1
+#define ACS_TOPO_CSR             2   /* user-supplied adjacency, see acs_create_csr (§8(f) row 1) */
 
 /* update rule (§A.7) */
 #define ACS_RULE_AVERAGE       0
@@ -134,6 +135,15 @@ typedef struct acs_result {
  * the fault schedule and x^0 on the device).  devices/n_devices: exactly one device id. */
 int acs_create(const acs_config* cfg, int backend, const int* devices, int n_devices,
                struct acs_sim** out);
+
+/* §8(f) row 1: a simulation on a user-supplied graph in CSR form (cfg->topology = ACS_TOPO_CSR;
+ * cfg->degree is ignored).  Receiver i's entries are itself (entry 0, no slot) followed by the
+ * senders colidx[rowptr[i] + t], t < deg(i) = rowptr[i+1] - rowptr[i], on slot s = rowptr[i] + t;
+ * m_i = deg(i) + 1 varies per receiver (trim rules need m_i > 2t for every i).  rowptr has N+1
+ * entries (rowptr[0] = 0, non-decreasing, rowptr[N] < 2^34), colidx rowptr[N] entries < N.
+ * Both arrays are copied to the device. */
+int acs_create_csr(const acs_config* cfg, const uint64_t* rowptr, const uint32_t* colidx, int device,
+                   struct acs_sim** out);
 
 /* §8(e) node partitioning of ONE RANDOM_REGULAR instance over n_ranks GPUs (cfg5), one process
  * (or thread) per GPU.  Rank r owns the 64-aligned row block [r*R, (r+1)*R) ∩ [0, N),

@@ -187,10 +187,18 @@ int acso_validate(const acs_config* c) {
             return fail(ACS_EINVAL, "degree must be even, in [2, 4096]");
         m = (uint64_t)c->degree + 1;
         slots = c->n_nodes * (uint64_t)c->degree;
+    } else if (c->topology == ACS_TOPO_CSR) {
+        m = 0;       /* per receiver: checked against the arrays by acso_create_csr */
+        slots = 0;
     } else {
         return fail(ACS_EINVAL, "unknown topology %u", c->topology);
     }
     if (slots >= (1ull << 34)) return fail(ACS_EINVAL, "slot count must be < 2^34");
+    if (c->topology == ACS_TOPO_CSR) {
+        if (c->rule > ACS_RULE_DLPSW_SELECT) return fail(ACS_EINVAL, "unknown rule %u", c->rule);
+        if (c->rule == ACS_RULE_AVERAGE && c->trim != 0) return fail(ACS_EINVAL, "AVERAGE requires trim == 0");
+        if (c->rule == ACS_RULE_DLPSW_SELECT && c->trim < 1) return fail(ACS_EINVAL, "DLPSW needs t >= 1");
+    } else
     switch (c->rule) {
         case ACS_RULE_AVERAGE:
             if (c->trim != 0) return fail(ACS_EINVAL, "AVERAGE requires trim == 0");
@@ -238,6 +246,8 @@ struct acso_sim {
     uint64_t N, B, m;
     uint32_t thr;            /* §A.5 drop threshold */
     uint32_t* nbr;           /* RANDOM_REGULAR: N*d neighbour ids (§A.3) */
+    uint64_t* rowptr;        /* CSR: N+1 row offsets (slot of entry 1+t of i = rowptr[i]+t) */
+    uint32_t* colidx;        /* CSR: rowptr[N] sender ids */
     uint32_t* status;        /* B*N: HONEST / BYZ / crash round (§A.4) */
     double* x;               /* B*N current values */
     double* xn;              /* B*N next values */
@@ -354,8 +364,59 @@ int acso_create(const acs_config* cfg, acso_sim** out) {
     return ACS_OK;
 }
 
+/* §8(f) row 1 / §A.3 (CSR extension): receiver i's entries are itself then the senders
+ * colidx[rowptr[i] + t] on slot rowptr[i] + t; m_i = deg(i) + 1. */
+int acso_create_csr(const acs_config* cfg, const uint64_t* rowptr, const uint32_t* colidx, acso_sim** out) {
+    if (!out) return fail(ACS_EINVAL, "null out");
+    *out = NULL;
+    if (!cfg || cfg->topology != ACS_TOPO_CSR) return fail(ACS_EINVAL, "config topology must be ACS_TOPO_CSR");
+    int rc = acso_validate(cfg);
+    if (rc) return rc;
+    if (!rowptr || !colidx) return fail(ACS_EINVAL, "null CSR arrays");
+    const uint64_t N = cfg->n_nodes;
+    if (rowptr[0] != 0) return fail(ACS_EINVAL, "rowptr[0] must be 0");
+    uint64_t mmax = 1;
+    for (uint64_t i = 0; i < N; ++i) {
+        if (rowptr[i + 1] < rowptr[i]) return fail(ACS_EINVAL, "rowptr must be non-decreasing");
+        const uint64_t m = rowptr[i + 1] - rowptr[i] + 1;
+        if (cfg->rule != ACS_RULE_AVERAGE && m <= 2ull * cfg->trim)
+            return fail(ACS_EINVAL, "receiver %llu has m = %llu <= 2t", (unsigned long long)i, (unsigned long long)m);
+        if (m > mmax) mmax = m;
+    }
+    const uint64_t nnz = rowptr[N];
+    if (nnz >= (1ull << 34)) return fail(ACS_EINVAL, "slot count must be < 2^34");
+    if (cfg->fault_model == ACS_FAULT_BYZANTINE && cfg->byz_strategy == ACS_BYZ_RANDOM && nnz > (1ull << 33))
+        return fail(ACS_EINVAL, "BYZ RANDOM needs slot count <= 2^33");
+    for (uint64_t k = 0; k < nnz; ++k)
+        if (colidx[k] >= N) return fail(ACS_EINVAL, "colidx[%llu] out of range", (unsigned long long)k);
+    acs_config c2 = *cfg;
+    c2.topology = ACS_TOPO_COMPLETE;   /* build everything but the graph through acso_create */
+    c2.n_nodes = N;
+    const uint32_t rule = c2.rule, trim = c2.trim;
+    c2.rule = ACS_RULE_AVERAGE;       /* topology-free validation of the rest */
+    c2.trim = 0;
+    if (N * N >= (1ull << 34)) c2.topology = ACS_TOPO_RANDOM_REGULAR, c2.degree = 2;
+    acso_sim* s = NULL;
+    rc = acso_create(&c2, &s);
+    if (rc) return rc;
+    free(s->nbr);
+    s->nbr = NULL;
+    s->c = *cfg;
+    s->c.rule = rule;
+    s->c.trim = trim;
+    s->m = mmax;
+    s->rowptr = (uint64_t*)malloc((N + 1) * sizeof(uint64_t));
+    s->colidx = (uint32_t*)malloc((nnz ? nnz : 1) * sizeof(uint32_t));
+    if (!s->rowptr || !s->colidx) { acso_destroy(s); return fail(ACS_ENOMEM, "oom"); }
+    memcpy(s->rowptr, rowptr, (N + 1) * sizeof(uint64_t));
+    memcpy(s->colidx, colidx, nnz * sizeof(uint32_t));
+    *out = s;
+    return ACS_OK;
+}
+
 void acso_destroy(acso_sim* s) {
     if (!s) return;
+    free(s->rowptr); free(s->colidx);
     free(s->nbr); free(s->status); free(s->x); free(s->xn); free(s->rounds); free(s->done);
     free(s->converged); free(s->lo); free(s->hi); free(s->trace);
     free(s);
@@ -414,6 +475,13 @@ static void step_instance(acso_sim* s, uint64_t lb) {
             if (c->topology == ACS_TOPO_COMPLETE) {
                 for (uint64_t j = 0; j < N; ++j)
                     S[j] = j == i ? x[i] : resolve(s, b, bG, r, x, st, i, j, i * N + j, lo, hi);
+            } else if (c->topology == ACS_TOPO_CSR) {
+                const uint64_t rp = s->rowptr[i], deg = s->rowptr[i + 1] - rp;
+                S[0] = x[i];
+                for (uint64_t t = 0; t < deg; ++t)
+                    S[1 + t] = resolve(s, b, bG, r, x, st, i, s->colidx[rp + t], rp + t, lo, hi);
+                xn[i] = apply_rule(c->rule, c->trim, S, deg + 1, scratch);
+                continue;
             } else {
                 const uint64_t d = c->degree;
                 S[0] = x[i];

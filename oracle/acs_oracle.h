@@ -36,6 +36,7 @@ int      acso_validate(const acs_config* cfg);
 
 /* simulation (§A.2–§A.9) */
 int  acso_create(const acs_config* cfg, acso_sim** out);
+int  acso_create_csr(const acs_config* cfg, const uint64_t* rowptr, const uint32_t* colidx, acso_sim** out);
 int  acso_round(acso_sim* sim, uint32_t k, acs_round_info* out);
 int  acso_run(acso_sim* sim, acs_result* out);
 int  acso_get_values(acso_sim* sim, uint64_t instance, double* out, uint64_t n);

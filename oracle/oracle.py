@@ -47,6 +47,7 @@ def load() -> C.CDLL:
         "acso_tree_sum": (C.c_double, [P(C.c_double), u64]),
         "acso_validate": (i32, [P(_abi.AcsConfig)]),
         "acso_create": (i32, [P(_abi.AcsConfig), P(vp)]),
+        "acso_create_csr": (i32, [P(_abi.AcsConfig), P(u64), P(u32), P(vp)]),
         "acso_round": (i32, [vp, u32, P(_abi.AcsRoundInfo)]),
         "acso_run": (i32, [vp, P(_abi.AcsResult)]),
         "acso_get_values": (i32, [vp, u64, P(C.c_double), u64]),
@@ -109,7 +110,7 @@ def validate(cfg: Config) -> int:
 class OracleSimulator:
     """Same surface as acsim.Simulator, backed by the CPU spec restatement."""
 
-    def __init__(self, cfg: Config | str, threads: int = 1):
+    def __init__(self, cfg: Config | str, threads: int = 1, csr=None):
         if isinstance(cfg, str):
             cfg = preset(cfg)
         if threads and not cfg.omp_threads:
@@ -118,7 +119,13 @@ class OracleSimulator:
         self._lib = load()
         self._c = cfg.to_c()
         h = C.c_void_p()
-        _chk(self._lib.acso_create(C.byref(self._c), C.byref(h)))
+        if csr is None:
+            _chk(self._lib.acso_create(C.byref(self._c), C.byref(h)))
+        else:
+            rp = np.ascontiguousarray(csr[0], dtype=np.uint64)
+            ci = np.ascontiguousarray(csr[1], dtype=np.uint32)
+            _chk(self._lib.acso_create_csr(C.byref(self._c), rp.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                           ci.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(h)))
         self._h = h
 
     def close(self):

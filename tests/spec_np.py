@@ -126,8 +126,11 @@ def apply_rule(rule: int, t: int, S: np.ndarray) -> np.ndarray:
 class NpSim:
     """Vectorised restatement of one configuration (attribute names as acsim.Config)."""
 
-    def __init__(self, cfg):
+    def __init__(self, cfg, csr=None):
         from acsim.config import _enum
+        if csr is not None:
+            self.rowptr = np.asarray(csr[0], dtype=np.int64)
+            self.colidx = np.asarray(csr[1], dtype=np.int64)
         self.cfg = cfg
         self.N = N = int(cfg.n_nodes)
         self.B = int(cfg.n_instances)
@@ -196,7 +199,17 @@ class NpSim:
         active = (st == HONEST) | (crash_node & (np.uint64(r) < st))
         A = np.nonzero(active)[0]
         xn = x.copy()
-        if A.size:
+        if A.size and self.topo == 2:
+            # CSR (§8(f) row 1): m_i varies, so receivers are resolved one row at a time
+            for i in A:
+                rp, re_ = int(self.rowptr[i]), int(self.rowptr[i + 1])
+                J = np.concatenate([[i], self.colidx[rp:re_]])[None, :]
+                slots = np.concatenate([[0], np.arange(rp, re_)]).astype(np.uint64)[None, :]
+                selfm = np.zeros(J.shape, dtype=bool)
+                selfm[0, 0] = True
+                V = self._values(np.array([i]), J, slots, selfm, r, b, bG, x, st, lo, hi)
+                xn[i] = apply_rule(self.rule, self.t, V)[0]
+        elif A.size:
             if self.topo == 0:
                 J = np.broadcast_to(np.arange(N), (A.size, N))
                 slots = A[:, None].astype(np.uint64) * np.uint64(N) + J.astype(np.uint64)
@@ -209,6 +222,16 @@ class NpSim:
                      A[:, None].astype(np.uint64) * np.uint64(self.d) + tt[None, :]], axis=1)
                 selfm = np.zeros(J.shape, dtype=bool)
                 selfm[:, 0] = True
+            V = self._values(A, J, slots, selfm, r, b, bG, x, st, lo, hi)
+            xn[A] = apply_rule(self.rule, self.t, V)
+        self.x[lb] = xn
+        self.rounds[lb] = r + 1
+        self._after(lb)
+
+    def _values(self, A, J, slots, selfm, r, b, bG, x, st, lo, hi):
+        """§A.6 resolution of the entry matrix (rows = receivers A, columns = entries)."""
+        cfg = self.cfg
+        if True:
             sj = st[J]
             cj = (sj != HONEST) & (sj != BYZ) & ~selfm
             missing = cj & (np.uint64(r) > sj)
@@ -232,10 +255,7 @@ class NpSim:
                     u = u53(draw(self.seed, BYZS, b, r, s2), draw(self.seed, BYZS, b, r, s2 + np.uint64(1)))
                     V[byzm] = (lo - d) + u * ((hi - lo) + 2.0 * d)
             V[missing | selfm] = np.broadcast_to(x[A][:, None], V.shape)[missing | selfm]
-            xn[A] = apply_rule(self.rule, self.t, V)
-        self.x[lb] = xn
-        self.rounds[lb] = r + 1
-        self._after(lb)
+        return V
 
     def round(self, k=1):
         for lb in range(self.B):
