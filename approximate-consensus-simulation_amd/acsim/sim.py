@@ -192,6 +192,10 @@ class Simulator:
         self._chk(self._lib.acs_get_kernel_timing(self._h, C.byref(ms), C.byref(n), name, 256))
         return ms.value, n.value, name.value.decode()
 
+    def kernel_name(self) -> str:
+        """Name of the round kernel(s) this handle's path launches."""
+        return self.kernel_timing()[2]
+
 
 def simulate(cfg: Config | str, backend: str = "hip", device: int = 0,
              devices: Optional[Sequence[int]] = None, return_values: bool = True,

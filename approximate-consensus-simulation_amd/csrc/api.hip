@@ -9,6 +9,7 @@
 #include <rccl/rccl.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -61,6 +62,8 @@ struct acs_sim {
     Path path = PATH_GENERIC;
     bool clean = true;
     bool ell_sorted = false;       // rows stored ascending (clean + order-independent rule)
+    bool binned = false;           // PATH_REGULAR served by the binned exchange (round_binned.hip)
+    BinnedPlan bin{};
     MsgParams mp{};
     double* x[2] = {nullptr, nullptr};
     uint32_t* ell = nullptr;       // rows [row0, row0 + rows_per) of this rank
@@ -187,6 +190,7 @@ static void release(acs_sim* s) {
     (void)hipFree(s->x[0]);
     (void)hipFree(s->x[1]);
     (void)hipFree(s->ell);
+    binned_free(s->bin);
     (void)hipFree(s->status);
     (void)hipFree(s->st);
     (void)hipFree(s->partial);
@@ -308,7 +312,9 @@ static int enqueue_round(acs_sim* s, uint32_t r) {
     int rc = timing_begin(s, &e1);
     if (rc) return rc;
     if (!s->partitioned) {
-        if (s->path == PATH_REGULAR) {
+        if (s->binned) {
+            HIP_TRY(launch_round_binned(s->bin, a, s->stream));
+        } else if (s->path == PATH_REGULAR) {
             HIP_TRY(launch_round_regular(a, s->B, s->clean, s->stream));
         } else if (s->path == PATH_DENSE) {
             DenseArgs d{};
@@ -571,8 +577,27 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         return fail(ACS_EUNSUPPORTED, "fault schedules need B*N < 2^31");
     }
     s->ell_sorted = s->path == PATH_REGULAR && s->clean && cfg->rule != ACS_RULE_AVERAGE;
+    // binned exchange: clean, order-independent rule, one instance, whole graph on this device,
+    // and tile runs long enough to stream (mean E / (P*Q) >= 16 deliveries)
+    uint32_t bin_sa = 8192;
+    if (const char* v = getenv("ACSIM_BIN_SA")) bin_sa = (uint32_t)strtoul(v, nullptr, 10);
+    if (bin_sa < 64 || bin_sa > 8192 || (bin_sa & (bin_sa - 1))) bin_sa = 8192;
+    {
+        const char* env = getenv("ACSIM_BINNED");
+        const bool allow = !(env && env[0] == '0');
+        const uint64_t P = (s->N + bin_sa - 1) / bin_sa, Q = (s->N + kBinSB - 1) / kBinSB;
+        const uint64_t E = s->N * (uint64_t)s->d;
+        s->binned = allow && s->path == PATH_REGULAR && s->clean && s->B == 1 && !partitioned &&
+                    binned_supported(s->d, cfg->trim, cfg->rule) && E < (1ull << 31) && E >= 16 * P * Q;
+        if (s->binned) {
+            char nm[96];
+            snprintf(nm, sizeof nm, "k_bin_scatter+k_bin_gather<%u,%u>", s->d, cfg->trim);
+            s->kname = nm;
+        }
+    }
     const uint64_t rows_local = partitioned ? s->rows_per : s->N;
-    s->nblk = s->path == PATH_REGULAR ? (uint32_t)((rows_local + kRegularBlock - 1) / kRegularBlock)
+    s->nblk = s->binned               ? (uint32_t)((s->N + kBinSB - 1) / kBinSB)
+            : s->path == PATH_REGULAR ? (uint32_t)((rows_local + kRegularBlock - 1) / kRegularBlock)
             : s->path == PATH_GENERIC ? (uint32_t)s->N
             : s->path == PATH_DENSE   ? dense_nblk(s->N)
                                       : 0u;
@@ -596,8 +621,8 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     CREATE_TRY(hipSetDevice(s->device));
     CREATE_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     const uint64_t xlen = s->B * s->Npad;
-    CREATE_TRY(hipMalloc(&s->x[0], xlen * sizeof(double)));
-    CREATE_TRY(hipMalloc(&s->x[1], xlen * sizeof(double)));
+    CREATE_TRY(hipMalloc(&s->x[0], (xlen + 2) * sizeof(double)));   // +2: 16-byte tail reads (binned)
+    CREATE_TRY(hipMalloc(&s->x[1], (xlen + 2) * sizeof(double)));
     CREATE_TRY(hipMalloc(&s->st, s->B * sizeof(InstState)));
     CREATE_TRY(hipMemsetAsync(s->st, 0, s->B * sizeof(InstState), s->stream));
     CREATE_TRY(hipMalloc(&s->partial, s->B * ncap * sizeof(double2)));
@@ -618,6 +643,13 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         CREATE_TRY(hipMalloc(&s->ell, words * sizeof(uint32_t)));
         CREATE_TRY(hipMemsetAsync(s->ell, 0, words * sizeof(uint32_t), s->stream));
         CREATE_TRY(build_rows(s, s->ell, partitioned ? rank : 0));
+        if (s->binned) {   // the plan replaces the ELL in the round loop
+            uint32_t chunks = 1;
+            if (const char* v = getenv("ACSIM_BIN_CHUNKS")) chunks = (uint32_t)strtoul(v, nullptr, 10);
+            CREATE_TRY(binned_build(s->bin, s->ell, s->N, s->d, s->dp, bin_sa, chunks, s->stream));
+            (void)hipFree(s->ell);
+            s->ell = nullptr;
+        }
         if (virt) {
             s->parts.resize(nranks - 1);
             for (int p = 1; p < nranks; ++p) {
@@ -869,7 +901,7 @@ int acs_get_fault_status(acs_sim* s, uint32_t* out, uint64_t n) {
 
 int acs_get_neighbors(acs_sim* s, uint32_t* out, uint64_t n) {
     if (!s || !out) return fail(ACS_EINVAL, "bad arguments");
-    if (!s->ell) return fail(ACS_EINVAL, "not a RANDOM_REGULAR topology");
+    if (s->c.topology != ACS_TOPO_RANDOM_REGULAR) return fail(ACS_EINVAL, "not a RANDOM_REGULAR topology");
     if (n < s->N * s->d) return fail(ACS_EINVAL, "buffer too small");
     HIP_TRY(hipSetDevice(s->device));
     // always rebuild the full graph in spec (slot) order on the side: the handle's own ELL may be

@@ -100,6 +100,33 @@ const char* regular_fast_name(uint32_t d, uint32_t t, bool clean);
 hipError_t launch_round_regular(const RoundArgs& a, uint64_t B, bool clean, hipStream_t s);
 constexpr uint32_t kRegularBlock = 256;
 
+// Binned exchange (round_binned.hip): the clean, order-independent RANDOM_REGULAR round as two
+// streaming kernels instead of N·d random 8-byte gathers.  Deliveries (i <- j) are grouped into
+// tiles (a, b) = (source block of SA senders, receiver block of kBinSB receivers), stored in
+// "A order" (a, b, i, slot).  Phase A (one LDS-resident source block per workgroup) streams
+// stage[p] = x[src(p)]; phase B (one receiver block per workgroup) reads its P tile runs into
+// LDS by LDS-DMA (concatenated), then every lane reads its d values through invpos and applies
+// the rule in registers.
+constexpr uint32_t kBinSB = 256;        // receivers per phase-B workgroup (one lane each)
+struct BinnedPlan {
+    uint32_t D = 0, SA = 0, P = 0, Q = 0, C = 1, segs = 0, chunk = 0;   // C: receiver-block chunks
+    uint64_t E = 0;                     // deliveries = N * D
+    uint64_t Ep = 0;                    // padded A-order length (tiles rounded up to even lengths)
+    uint16_t* idxA = nullptr;           // [Ep] A order: sender index within its source block (0 in pads)
+    uint16_t* invpos = nullptr;         // [Q][D/8][kBinSB][8]: position of (receiver, slot) in block b's runs
+    uint2* tiles = nullptr;             // [Q][P+1] (A-order start, element offset in block b's runs)
+    uint64_t* aoffc = nullptr;          // [P][C+1] A-order start of (source block a, chunk c)
+    double* stage = nullptr;            // [Ep] A order: the delivered values
+};
+bool binned_supported(uint32_t d, uint32_t t, uint32_t rule);
+// Builds the plan from a (sorted or spec-order) ELL of all N rows; sa = source block size.
+// chunks > 1 splits every round into per-chunk (A, B) launch pairs over receiver-block ranges,
+// so one chunk's staging can stay in the 256 MiB Infinity Cache between its two phases.
+hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint32_t d, uint32_t dp, uint32_t sa,
+                        uint32_t chunks, hipStream_t s);
+void binned_free(BinnedPlan& p);
+hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, hipStream_t s);
+
 // Generic kernel: one workgroup per receiver, LDS bitonic sort (any topology, m <= 8192).
 constexpr uint32_t kGenericMaxM = 8192;
 hipError_t launch_round_generic(const RoundArgs& a, uint64_t B, hipStream_t s);

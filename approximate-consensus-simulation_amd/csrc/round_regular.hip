@@ -13,27 +13,9 @@
 // Algorithmic traffic (no faults, no loss): 4D + 8D + 8 + 8 bytes per node-round (400 B at
 // D = 32).  Everything is bit-exact with the spec: no FMA (-ffp-contract=off), IEEE division.
 #include "resolve.hpp"
-#include "sortnet.hpp"
+#include "rules.hpp"
 
 namespace acs {
-
-template <int D, int T>
-__device__ __forceinline__ double apply_rule_reg(uint32_t rule, double (&v)[D + 1]) {
-    constexpr int M = D + 1;
-    if constexpr (T == 0) {
-        if (rule == 0) return tree_sum_const<M>(v) / (double)M;   // AVERAGE: entry order
-    }
-    select_sort<M, T, M - T>(v);
-    constexpr int NR = M - 2 * T;
-    if (rule == 2) return (v[T] + v[M - T - 1]) * 0.5;                // MIDPOINT
-    if constexpr (T >= 1) {
-        if (rule == 3) {                                             // DLPSW: R[0], R[T], ...
-            constexpr int NQ = (NR + T - 1) / T;
-            return tree_sum_const<NQ, T, T>(v) / (double)NQ;
-        }
-    }
-    return tree_sum_const<NR, T>(v) / (double)NR;                    // TRIMMED_MEAN
-}
 
 template <int D, int T, bool CLEAN>
 __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs a) {

@@ -214,4 +214,4 @@ def test_kernel_timing_counts_round_launches():
         s.set_kernel_timing(True)
         s.run()
         ms, n, name = s.kernel_timing()
-        assert n == 12 and ms > 0 and name.startswith("k_round_regular<32,5")
+        assert n == 12 and ms > 0 and (name.startswith("k_round_regular<32,5") or name.startswith("k_bin_scatter+k_bin_gather<32,5>"))
