@@ -579,9 +579,9 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     s->ell_sorted = s->path == PATH_REGULAR && s->clean && cfg->rule != ACS_RULE_AVERAGE;
     // binned exchange: clean, order-independent rule, one instance, whole graph on this device,
     // and tile runs long enough to stream (mean E / (P*Q) >= 16 deliveries)
-    uint32_t bin_sa = 8192;
+    uint32_t bin_sa = 16384;
     if (const char* v = getenv("ACSIM_BIN_SA")) bin_sa = (uint32_t)strtoul(v, nullptr, 10);
-    if (bin_sa < 64 || bin_sa > 8192 || (bin_sa & (bin_sa - 1))) bin_sa = 8192;
+    if (bin_sa < 64 || bin_sa > 16384 || (bin_sa & (bin_sa - 1))) bin_sa = 16384;
     {
         const char* env = getenv("ACSIM_BINNED");
         const bool allow = !(env && env[0] == '0');

@@ -29,7 +29,9 @@ namespace acs {
 // ------------------------------------------------------------------------------ phase A
 // aoffc[a][c] (C+1 per a): A-order start of tile (a, first receiver block of chunk c); the
 // launch for chunk c covers [aoffc[a][c], aoffc[a][c+1]) of every source block a.
-__global__ __launch_bounds__(256) void k_bin_scatter(const double* __restrict__ x, const uint16_t* __restrict__ idxA,
+constexpr uint32_t kBinA = 512;   // phase-A workgroup: 8 waves streaming one LDS-resident source block
+
+__global__ __launch_bounds__(kBinA) void k_bin_scatter(const double* __restrict__ x, const uint16_t* __restrict__ idxA,
                                                      const uint64_t* __restrict__ aoffc, double* __restrict__ stage,
                                                      const InstState* __restrict__ st, uint64_t N, uint32_t SA,
                                                      uint32_t segs, uint32_t chunk, uint32_t C, uint32_t c) {
@@ -47,30 +49,31 @@ __global__ __launch_bounds__(256) void k_bin_scatter(const double* __restrict__ 
         const uint32_t n16 = (n + 1) / 2;
         const uint4* xs = reinterpret_cast<const uint4*>(x + base) + threadIdx.x;
         uint4* ld = reinterpret_cast<uint4*>(lx) + (threadIdx.x & ~63u);
-        for (uint32_t o = 0; o < n16; o += 256)
+        for (uint32_t o = 0; o < n16; o += kBinA)
             if (o + threadIdx.x < n16) __builtin_amdgcn_global_load_lds(xs + o, ld + o, 16, 0, 0);
     }
     __syncthreads();
 
-    // super-steps of 2048 positions: wave w takes [w*512, w*512+512); instruction q of a lane
-    // covers positions q*128 + 2*lane, +1 (one u32 of two indices, one 16-byte store)
+    // super-steps of 512 positions per wave: wave w takes [w*512, w*512+512); instruction q of a
+    // lane covers positions q*128 + 2*lane, +1 (one u32 of two indices, one 16-byte store)
+    constexpr uint32_t SUP = kBinA / 64 * 512, SUPW = SUP / 2;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint64_t p = p0;
     if ((p0 & 1) == 0) {
-        const uint64_t nsup = (p1 - p0) / 2048;
+        const uint64_t nsup = (p1 - p0) / SUP;
         const uint32_t* ip = reinterpret_cast<const uint32_t*>(idxA + p0) + w * 256 + lane;
         double2* op = reinterpret_cast<double2*>(stage + p0) + w * 256 + lane;
 #pragma unroll 4
         for (uint64_t k = 0; k < nsup; ++k) {
             uint32_t c[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) c[q] = __builtin_nontemporal_load(ip + k * 1024 + q * 64);
+            for (int q = 0; q < 4; ++q) c[q] = __builtin_nontemporal_load(ip + k * SUPW + q * 64);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) op[k * 1024 + q * 64] = make_double2(lx[c[q] & 0xFFFFu], lx[c[q] >> 16]);
+            for (int q = 0; q < 4; ++q) op[k * SUPW + q * 64] = make_double2(lx[c[q] & 0xFFFFu], lx[c[q] >> 16]);
         }
-        p = p0 + nsup * 2048;
+        p = p0 + nsup * SUP;
     }
-    for (uint64_t q = p + threadIdx.x; q < p1; q += 256) stage[q] = lx[idxA[q]];
+    for (uint64_t q = p + threadIdx.x; q < p1; q += kBinA) stage[q] = lx[idxA[q]];
 }
 
 // ------------------------------------------------------------------------------ phase B
@@ -274,7 +277,7 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint32_t
     // deliveries per phase-A workgroup (multiple of 2048); a chunk's share of one source block
     // is about sa*d/C, so segs covers it with slack for the binomial spread of tile sizes
     p.chunk = 65536 / p.C < 8192 ? 8192 : 65536 / p.C;
-    p.chunk = (p.chunk + 2047) / 2048 * 2048;
+    p.chunk = (p.chunk + 4095) / 4096 * 4096;
     p.segs = 1;   // set from the real per-(a, c) range lengths once aoffc is built
     const uint64_t E = p.E, nt = (uint64_t)p.P * p.Q;
     if (E >= (1ull << 31) || nt >= (1ull << 32)) return hipErrorNotSupported;
@@ -357,8 +360,15 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint32_t
 }
 
 hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, hipStream_t s) {
+    static bool attr = false;   // source blocks above 8192 senders need more than 64 KiB of LDS
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_scatter),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 16384 * sizeof(double));
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
     for (uint32_t c = 0; c < p.C; ++c) {
-        hipLaunchKernelGGL(k_bin_scatter, dim3(p.P * p.segs), dim3(256), p.SA * sizeof(double), s, a.xin, p.idxA,
+        hipLaunchKernelGGL(k_bin_scatter, dim3(p.P * p.segs), dim3(kBinA), p.SA * sizeof(double), s, a.xin, p.idxA,
                            p.aoffc, p.stage, a.st, a.N, p.SA, p.segs, p.chunk, p.C, c);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;

@@ -80,8 +80,20 @@ struct SelectNet {
     static constexpr int count = list.n;
 };
 
-__device__ __forceinline__ double ce_min(double a, double b) { return __builtin_fmin(a, b); }
-__device__ __forceinline__ double ce_max(double a, double b) { return __builtin_fmax(a, b); }
+// fp64 compare-exchange halves as raw v_min_f64 / v_max_f64: every value the engine sorts is a
+// finite, non-NaN double (inputs are validated), so the sNaN-quieting canonicalisation that
+// __builtin_fmin / fmax add for values loaded from memory (one extra v_max_f64 per input) is dead
+// work.  -0.0 never occurs (§A.4 canonicalises the constant), so min/max are exact.
+__device__ __forceinline__ double ce_min(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double ce_max(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 __device__ __forceinline__ uint32_t ce_min(uint32_t a, uint32_t b) { return a < b ? a : b; }
 __device__ __forceinline__ uint32_t ce_max(uint32_t a, uint32_t b) { return a < b ? b : a; }
 

@@ -7,10 +7,14 @@ launches one rank per GPU with torch.distributed.run: cfg4 does not shard (SURVE
 only), so each rank runs its own independent instance (global instance id = rank; same graph)
 and `value` is the whole-node aggregate: N·n_nodes·K ÷ max-over-ranks time ("scaling": "weak").
 
-The roofline object prices the dominant kernel (the round kernel) at SURVEY §8(d)'s algorithmic
-400 B/node-round (32·4 B column ids + 32·8 B neighbour values + 8 B own value + 8 B store) times
-the N nodes one launch processes, divided by its average device duration measured with HIP
-events on the handle's stream over the timed region.  cpu_baseline times the CPU oracle (this
+The roofline object prices the dominant kernel at SURVEY §8(d)'s algorithmic 400 B/node-round
+(32·4 B column ids + 32·8 B neighbour values + 8 B own value + 8 B store) times the N nodes one
+launch processes, divided by its average device duration measured with HIP events on the
+handle's stream over the timed region.  On cfg4 the round is the binned exchange
+(csrc/round_binned.hip): two launches, k_bin_scatter then k_bin_gather, bracketed together by
+one event pair per round, so "one launch" here means that pair (the ε finalize is excluded).
+`traffic` is the pair's measured HBM bytes per round (profiles/pmc_cfg4.json, FETCH_SIZE x 2 +
+WRITE_SIZE, tools/traffic_json.py).  cpu_baseline times the CPU oracle (this
 repo's spec restatement, oracle/) on rank 0 on a bounded sample of the same workload.
 """
 from __future__ import annotations
