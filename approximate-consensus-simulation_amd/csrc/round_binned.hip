@@ -274,10 +274,15 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint32_t
     p.P = (uint32_t)((N + sa - 1) / sa);
     p.Q = (uint32_t)((N + kBinSB - 1) / kBinSB);
     p.C = chunks < 1 ? 1 : chunks > p.Q ? p.Q : chunks;
-    // deliveries per phase-A workgroup (multiple of 2048); a chunk's share of one source block
-    // is about sa*d/C, so segs covers it with slack for the binomial spread of tile sizes
-    p.chunk = 65536 / p.C < 8192 ? 8192 : 65536 / p.C;
-    p.chunk = (p.chunk + 4095) / 4096 * 4096;
+    // deliveries per phase-A workgroup (a multiple of the 4096-position super-step): about 512
+    // workgroups per launch (two generations per CU measured faster than one), few x-block refills
+    {
+        const uint64_t per_a = ((uint64_t)sa * d + p.C - 1) / p.C;
+        const uint64_t want = (512 + p.P - 1) / p.P;
+        uint64_t ch = (per_a + want - 1) / want;
+        ch = ch < 8192 ? 8192 : ch;
+        p.chunk = (uint32_t)((ch + 4095) / 4096 * 4096);
+    }
     p.segs = 1;   // set from the real per-(a, c) range lengths once aoffc is built
     const uint64_t E = p.E, nt = (uint64_t)p.P * p.Q;
     if (E >= (1ull << 31) || nt >= (1ull << 32)) return hipErrorNotSupported;
