@@ -51,6 +51,7 @@ enum Path { PATH_REGULAR = 0, PATH_GENERIC = 1, PATH_BATCHED = 2, PATH_DENSE = 3
 struct Part {              // one node partition's private copy (virtual partitions only)
     double* x[2] = {nullptr, nullptr};
     uint32_t* ell = nullptr;
+    BinnedPlan bin{};
 };
 
 struct acs_sim {
@@ -186,6 +187,7 @@ static void release(acs_sim* s) {
         (void)hipFree(p.x[0]);
         (void)hipFree(p.x[1]);
         (void)hipFree(p.ell);
+        binned_free(p.bin);
     }
     (void)hipFree(s->x[0]);
     (void)hipFree(s->x[1]);
@@ -357,7 +359,10 @@ static int enqueue_round(acs_sim* s, uint32_t r) {
             ap.nrows = part_rows(s, p);
             ap.partial = s->partial + (uint64_t)p * s->nblk;
             if (ap.nrows == 0) continue;   // empty tail partition (its partials are not folded)
-            HIP_TRY(launch_round_regular(ap, s->B, s->clean, s->stream));
+            if (s->binned)
+                HIP_TRY(launch_round_binned(p == 0 ? s->bin : s->parts[p - 1].bin, ap, s->stream));
+            else
+                HIP_TRY(launch_round_regular(ap, s->B, s->clean, s->stream));
         }
         if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
         // all-gather emulation: copy each partition's fresh rows into every other copy
@@ -381,7 +386,12 @@ static int enqueue_round(acs_sim* s, uint32_t r) {
     // RCCL partition: own rows, then in-place all-gather of x^{r+1} and all-reduce of the spread
     a.row0 = part_row0(s, s->rank);
     a.nrows = part_rows(s, s->rank);
-    if (a.nrows) HIP_TRY(launch_round_regular(a, s->B, s->clean, s->stream));
+    if (a.nrows) {
+        if (s->binned)
+            HIP_TRY(launch_round_binned(s->bin, a, s->stream));
+        else
+            HIP_TRY(launch_round_regular(a, s->B, s->clean, s->stream));
+    }
     if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
     double* xo = s->x[(r + 1) & 1u];
     NCCL_TRY(ncclAllGather(xo + a.row0, xo, s->rows_per, ncclFloat64, s->comm, s->stream));
@@ -577,27 +587,27 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         return fail(ACS_EUNSUPPORTED, "fault schedules need B*N < 2^31");
     }
     s->ell_sorted = s->path == PATH_REGULAR && s->clean && cfg->rule != ACS_RULE_AVERAGE;
-    // binned exchange: clean, order-independent rule, one instance, whole graph on this device,
-    // and tile runs long enough to stream (mean E / (P*Q) >= 16 deliveries)
+    const uint64_t rows_local = partitioned ? s->rows_per : s->N;
+    // binned exchange (round_binned.hip): clean, order-independent rule, one instance, and a graph
+    // shape with one or two exchange levels; ACSIM_BINNED=0 forces the per-lane kernel and
+    // ACSIM_BIN_SA sets the source block size (tests use small blocks on small graphs)
     uint32_t bin_sa = 16384;
     if (const char* v = getenv("ACSIM_BIN_SA")) bin_sa = (uint32_t)strtoul(v, nullptr, 10);
     if (bin_sa < 64 || bin_sa > 16384 || (bin_sa & (bin_sa - 1))) bin_sa = 16384;
     {
         const char* env = getenv("ACSIM_BINNED");
         const bool allow = !(env && env[0] == '0');
-        const uint64_t P = (s->N + bin_sa - 1) / bin_sa, Q = (s->N + kBinSB - 1) / kBinSB;
-        const uint64_t E = s->N * (uint64_t)s->d;
-        s->binned = allow && s->path == PATH_REGULAR && s->clean && s->B == 1 && !partitioned &&
-                    binned_supported(s->d, cfg->trim, cfg->rule) && E < (1ull << 31) && E >= 16 * P * Q;
+        const uint32_t lv = s->path == PATH_REGULAR && s->d ? binned_levels(s->N, rows_local, s->d, bin_sa, nullptr) : 0;
+        s->binned = allow && s->path == PATH_REGULAR && s->clean && s->B == 1 && lv != 0 &&
+                    binned_supported(s->d, cfg->trim, cfg->rule) && rows_local * s->d < (1ull << 32);
         if (s->binned) {
             char nm[96];
-            snprintf(nm, sizeof nm, "k_bin_scatter+k_bin_gather<%u,%u>", s->d, cfg->trim);
+            snprintf(nm, sizeof nm, "k_bin_scatter+%sk_bin_gather<%u,%u>", lv == 2 ? "k_bin_regroup+" : "", s->d,
+                     cfg->trim);
             s->kname = nm;
         }
     }
-    const uint64_t rows_local = partitioned ? s->rows_per : s->N;
-    s->nblk = s->binned               ? (uint32_t)((s->N + kBinSB - 1) / kBinSB)
-            : s->path == PATH_REGULAR ? (uint32_t)((rows_local + kRegularBlock - 1) / kRegularBlock)
+    s->nblk = s->path == PATH_REGULAR ? (uint32_t)((rows_local + kRegularBlock - 1) / kRegularBlock)
             : s->path == PATH_GENERIC ? (uint32_t)s->N
             : s->path == PATH_DENSE   ? dense_nblk(s->N)
                                       : 0u;
@@ -644,9 +654,8 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         CREATE_TRY(hipMemsetAsync(s->ell, 0, words * sizeof(uint32_t), s->stream));
         CREATE_TRY(build_rows(s, s->ell, partitioned ? rank : 0));
         if (s->binned) {   // the plan replaces the ELL in the round loop
-            uint32_t chunks = 1;
-            if (const char* v = getenv("ACSIM_BIN_CHUNKS")) chunks = (uint32_t)strtoul(v, nullptr, 10);
-            CREATE_TRY(binned_build(s->bin, s->ell, s->N, s->d, s->dp, bin_sa, chunks, s->stream));
+            const uint64_t nr = partitioned ? part_rows(s, rank) : s->N;
+            if (nr) CREATE_TRY(binned_build(s->bin, s->ell, s->N, nr, s->d, s->dp, bin_sa, s->stream));
             (void)hipFree(s->ell);
             s->ell = nullptr;
         }
@@ -654,11 +663,17 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
             s->parts.resize(nranks - 1);
             for (int p = 1; p < nranks; ++p) {
                 Part& q = s->parts[p - 1];
-                CREATE_TRY(hipMalloc(&q.x[0], xlen * sizeof(double)));
-                CREATE_TRY(hipMalloc(&q.x[1], xlen * sizeof(double)));
+                CREATE_TRY(hipMalloc(&q.x[0], (xlen + 2) * sizeof(double)));
+                CREATE_TRY(hipMalloc(&q.x[1], (xlen + 2) * sizeof(double)));
                 CREATE_TRY(hipMalloc(&q.ell, words * sizeof(uint32_t)));
                 CREATE_TRY(hipMemsetAsync(q.ell, 0, words * sizeof(uint32_t), s->stream));
                 CREATE_TRY(build_rows(s, q.ell, p));
+                if (s->binned) {
+                    const uint64_t nr = part_rows(s, p);
+                    if (nr) CREATE_TRY(binned_build(q.bin, q.ell, s->N, nr, s->d, s->dp, bin_sa, s->stream));
+                    (void)hipFree(q.ell);
+                    q.ell = nullptr;
+                }
             }
         }
     }

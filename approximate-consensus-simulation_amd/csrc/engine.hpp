@@ -100,30 +100,35 @@ const char* regular_fast_name(uint32_t d, uint32_t t, bool clean);
 hipError_t launch_round_regular(const RoundArgs& a, uint64_t B, bool clean, hipStream_t s);
 constexpr uint32_t kRegularBlock = 256;
 
-// Binned exchange (round_binned.hip): the clean, order-independent RANDOM_REGULAR round as two
+// Binned exchange (round_binned.hip): the clean, order-independent RANDOM_REGULAR round as
 // streaming kernels instead of N·d random 8-byte gathers.  Deliveries (i <- j) are grouped into
-// tiles (a, b) = (source block of SA senders, receiver block of kBinSB receivers), stored in
-// "A order" (a, b, i, slot).  Phase A (one LDS-resident source block per workgroup) streams
-// stage[p] = x[src(p)]; phase B (one receiver block per workgroup) reads its P tile runs into
-// LDS by LDS-DMA (concatenated), then every lane reads its d values through invpos and applies
-// the rule in registers.
+// tiles of (source block of SA senders, receiver group) and stored with tiles padded to even
+// lengths.  Phase A (an LDS-resident source block per workgroup) streams stage1[p] = x[src(p)];
+// for two-level plans phase M regroups stage1 by receiver block into stage2; phase B (one
+// receiver block per workgroup) copies its runs into LDS by LDS-DMA, then every lane reads its d
+// values through invpos and applies the rule in registers.
 constexpr uint32_t kBinSB = 256;        // receivers per phase-B workgroup (one lane each)
 struct BinnedPlan {
-    uint32_t D = 0, SA = 0, P = 0, Q = 0, C = 1, segs = 0, chunk = 0;   // C: receiver-block chunks
-    uint64_t E = 0;                     // deliveries = N * D
-    uint64_t Ep = 0;                    // padded A-order length (tiles rounded up to even lengths)
-    uint16_t* idxA = nullptr;           // [Ep] A order: sender index within its source block (0 in pads)
+    uint32_t D = 0, SA = 0, P = 0, Q = 0, levels = 0, PK = 0, ngroups = 0, nrun = 0, mcap = 0;
+    uint32_t segs = 0, chunk = 0;       // phase-A workgroups per source block, deliveries per workgroup
+    uint64_t E = 0;                     // deliveries = local rows * D
+    uint64_t Ep1 = 0, Ep2 = 0;          // padded stage lengths
+    uint16_t* idxA = nullptr;           // [Ep1] sender index within its source block (0 in pads)
+    uint16_t* idxM = nullptr;           // [Ep2] position inside the phase-M LDS image (two levels)
     uint16_t* invpos = nullptr;         // [Q][D/8][kBinSB][8]: position of (receiver, slot) in block b's runs
-    uint2* tiles = nullptr;             // [Q][P+1] (A-order start, element offset in block b's runs)
-    uint64_t* aoffc = nullptr;          // [P][C+1] A-order start of (source block a, chunk c)
-    double* stage = nullptr;            // [Ep] A order: the delivered values
+    uint2* tiles = nullptr;             // [Q][nrun+1] (stage start, element offset in block b's runs)
+    uint2* mt = nullptr;                // [ngroups][PK+1] phase-M run tables (two levels)
+    uint64_t* aoff = nullptr;           // [P+1] stage1 start of source block a
+    uint64_t* moff = nullptr;           // [ngroups+1] stage2 start of phase-M group g
+    double* stage1 = nullptr;           // [Ep1]
+    double* stage2 = nullptr;           // [Ep2] (two levels)
 };
 bool binned_supported(uint32_t d, uint32_t t, uint32_t rule);
-// Builds the plan from a (sorted or spec-order) ELL of all N rows; sa = source block size.
-// chunks > 1 splits every round into per-chunk (A, B) launch pairs over receiver-block ranges,
-// so one chunk's staging can stay in the 256 MiB Infinity Cache between its two phases.
-hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint32_t d, uint32_t dp, uint32_t sa,
-                        uint32_t chunks, hipStream_t s);
+// 1 or 2 exchange levels for NR local receivers of an N-node graph (0: not supported).
+uint32_t binned_levels(uint64_t N, uint64_t NR, uint32_t d, uint32_t sa, uint32_t* sr_out);
+// Builds the plan from the ELL of the NR local rows (sorted or spec order); sa = source block size.
+hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t NR, uint32_t d, uint32_t dp,
+                        uint32_t sa, hipStream_t s);
 void binned_free(BinnedPlan& p);
 hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, hipStream_t s);
 

@@ -1,18 +1,22 @@
-// round_binned.hip — the headline round (SURVEY §8(a) a5+a7+a8+a9, cfg4) as a binned exchange.
+// round_binned.hip — the sparse round (SURVEY §8(a) a5+a7+a8+a9: cfg4, cfg5) as a binned exchange.
 //
 // Why: the per-lane kernel (round_regular.hip) issues N·d random 8-byte gathers per round.  On
-// MI355X each one moves a whole cache line from L2 (or MALL, when x outgrows one XCD's 4 MiB L2)
-// into L1, so the round is bound by line traffic, not by the 400 algorithmic bytes per node
-// (DESIGN.md §5).  Here every HBM access is a coalesced stream and the only random accesses
-// are 8-byte LDS accesses:
+// MI355X each one moves a whole cache line into L1 (from L2 / MALL at cfg4, from HBM at cfg5), so
+// the round is bound by line traffic, not by the algorithmic bytes per node.  Here
+// every HBM access is a coalesced stream or a ≥ 1 KiB run, and the only random accesses are
+// 8-byte LDS accesses.  A "delivery" is one (receiver i <- sender j, slot t) entry.
 //
 //   phase A  k_bin_scatter   workgroup = (source block a of SA senders, segment of its deliveries)
-//            x[a·SA, (a+1)·SA) -> LDS (one coalesced read), then a pure stream over the block's
-//            deliveries in A order: stage[p] = lds[idxA[p]].           2 B read + 8 B write / delivery
+//            x[a·SA, (a+1)·SA) -> LDS by LDS-DMA, then a pure stream over the block's deliveries:
+//            stage1[p] = lds[idxA[p]]                                  2 B read + 8 B write / delivery
+//   phase M  k_bin_regroup   (two-level plans only: cfg5-sized graphs, where a (source block,
+//            receiver block) tile would hold about one delivery)  workgroup = (receiver
+//            super-block r, source-block chunk k): its PK runs of stage1 -> LDS by LDS-DMA, then
+//            stage2[p] = lds[idxM[p]] grouped by receiver block         8 B + 2 B read + 8 B write
 //   phase B  k_bin_gather    workgroup = receiver block b of kBinSB receivers (one lane each)
-//            its P tile runs (a, b) of stage -> LDS by LDS-DMA, then per lane: own x_i, its d
-//            values at invpos (LDS), the §A.7 rule in registers (rules.hpp), one store, block
-//            (min, max) partial.                                       8 B + 2 B read / delivery
+//            its runs of the last stage -> LDS by LDS-DMA, then per lane: own x_i, its d values at
+//            invpos (LDS), the §A.7 rule in registers (rules.hpp), one store, block (min, max)
+//            partial.                                                  8 B + 2 B read / delivery
 //
 // Only clean configs with an order-independent rule (TRIMMED / MIDPOINT / DLPSW) take this path:
 // the rule depends on the multiset of received values only, so the slot a value lands in does
@@ -26,43 +30,22 @@
 
 namespace acs {
 
-// ------------------------------------------------------------------------------ phase A
-// aoffc[a][c] (C+1 per a): A-order start of tile (a, first receiver block of chunk c); the
-// launch for chunk c covers [aoffc[a][c], aoffc[a][c+1]) of every source block a.
-constexpr uint32_t kBinA = 512;   // phase-A workgroup: 8 waves streaming one LDS-resident source block
+constexpr uint32_t kBinA = 512;        // phase-A / phase-M workgroup: 8 waves
+constexpr uint32_t kBinMCap = 19456;   // phase-M LDS image capacity (elements, 152 KiB)
 
-__global__ __launch_bounds__(kBinA) void k_bin_scatter(const double* __restrict__ x, const uint16_t* __restrict__ idxA,
-                                                     const uint64_t* __restrict__ aoffc, double* __restrict__ stage,
-                                                     const InstState* __restrict__ st, uint64_t N, uint32_t SA,
-                                                     uint32_t segs, uint32_t chunk, uint32_t C, uint32_t c) {
-    extern __shared__ double lx[];
-    if (st->done) return;
-    const uint32_t a = blockIdx.x / segs, sg = blockIdx.x % segs;
-    const uint64_t pa1 = aoffc[(uint64_t)a * (C + 1) + c + 1];
-    const uint64_t p0 = aoffc[(uint64_t)a * (C + 1) + c] + (uint64_t)sg * chunk;
-    if (p0 >= pa1) return;
-    const uint64_t p1 = p0 + chunk < pa1 ? p0 + chunk : pa1;
-    const uint64_t base = (uint64_t)a * SA;
-    const uint32_t n = (uint32_t)(N - base < SA ? N - base : SA);
-    {   // x block -> LDS by LDS-DMA, 16 B per lane (x is allocated with one spare element, so the
-        // last odd element's pair never reads past the buffer)
-        const uint32_t n16 = (n + 1) / 2;
-        const uint4* xs = reinterpret_cast<const uint4*>(x + base) + threadIdx.x;
-        uint4* ld = reinterpret_cast<uint4*>(lx) + (threadIdx.x & ~63u);
-        for (uint32_t o = 0; o < n16; o += kBinA)
-            if (o + threadIdx.x < n16) __builtin_amdgcn_global_load_lds(xs + o, ld + o, 16, 0, 0);
-    }
-    __syncthreads();
-
-    // super-steps of 512 positions per wave: wave w takes [w*512, w*512+512); instruction q of a
-    // lane covers positions q*128 + 2*lane, +1 (one u32 of two indices, one 16-byte store)
+// ------------------------------------------------------------------------------ shared pieces
+// Stream [p0, p1) of an index stream: out[p] = lds[idx[p]].  Super-steps of 512 positions per
+// wave; instruction q of a lane covers positions q*128 + 2*lane, +1 (one u32 of two indices, one
+// 16-byte store), so every wave-instruction reads 256 B and writes 1 KiB contiguously.
+__device__ __forceinline__ void bin_stream(const double* lx, const uint16_t* __restrict__ idx, double* __restrict__ out,
+                                           uint64_t p0, uint64_t p1) {
     constexpr uint32_t SUP = kBinA / 64 * 512, SUPW = SUP / 2;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint64_t p = p0;
     if ((p0 & 1) == 0) {
         const uint64_t nsup = (p1 - p0) / SUP;
-        const uint32_t* ip = reinterpret_cast<const uint32_t*>(idxA + p0) + w * 256 + lane;
-        double2* op = reinterpret_cast<double2*>(stage + p0) + w * 256 + lane;
+        const uint32_t* ip = reinterpret_cast<const uint32_t*>(idx + p0) + w * 256 + lane;
+        double2* op = reinterpret_cast<double2*>(out + p0) + w * 256 + lane;
 #pragma unroll 4
         for (uint64_t k = 0; k < nsup; ++k) {
             uint32_t c[4];
@@ -73,44 +56,18 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const double* __restrict_
         }
         p = p0 + nsup * SUP;
     }
-    for (uint64_t q = p + threadIdx.x; q < p1; q += kBinA) stage[q] = lx[idxA[q]];
+    for (uint64_t q = p + threadIdx.x; q < p1; q += blockDim.x) out[q] = lx[idx[q]];
 }
 
-// ------------------------------------------------------------------------------ phase B
-// The P tile runs of block b are copied global -> LDS by LDS-DMA (global_load_lds, no VGPR
-// staging, so a wave keeps all its runs in flight), concatenated in a order: run a lands at
-// element pre(a, b).  Lane i_local then reads its D values at invpos[b][t][i_local].
-template <int D, int T>
-__global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const double* __restrict__ stage,
-                                                       const uint16_t* __restrict__ invpos,
-                                                       const uint2* __restrict__ tiles, uint32_t P, uint32_t b0,
-                                                       uint32_t b1, uint32_t Qc) {
-    static_assert(D % 8 == 0, "invpos is read 8 slots at a time");
-    // runs are padded to even lengths; P <= D*kBinSB/16 (binned_supported's mean-run bound)
-    __shared__ __attribute__((aligned(16))) double raw[D * kBinSB + D * kBinSB / 16];
-    InstState* S = a.st;
-    if (S->done) return;
-    // XCD-aware order: consecutive receiver blocks (which share the lines at their tile-run
-    // seams) run on the same XCD (dispatch is round-robin over the 8 XCDs by blockIdx)
-    const uint32_t b = b0 + (blockIdx.x & 7u) * Qc + (blockIdx.x >> 3);
-    if (b >= b1) return;
+// Copy runs [r0, r1) of a run table (start in `src` elements, element offset `pre` in the LDS
+// image; run k ends where run k+1's image begins) into LDS by 16-byte LDS-DMA.  Every run is
+// padded to an even length, so starts are 16-byte aligned on both sides.  Descriptors are fetched
+// one per lane, 64 at a time, and broadcast with readlane: no run waits on a dependent load.
+__device__ __forceinline__ void bin_dma_runs(const uint2* __restrict__ tb, uint32_t r0, uint32_t r1,
+                                             const double* __restrict__ src, double* dst) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t i = (uint64_t)b * kBinSB + threadIdx.x;
-    const bool live = i < a.N;
-    // ordinary loads first (their wait is the barrier's vmcnt(0) anyway)
-    const double xi = live ? a.xin[i] : 0.0;
-    uint4 ip[D / 8];
-    const uint4* ipp = reinterpret_cast<const uint4*>(invpos) + (uint64_t)b * (D / 8) * kBinSB + threadIdx.x;
-#pragma unroll
-    for (int q = 0; q < D / 8; ++q) ip[q] = ipp[q * kBinSB];
-    // wave w copies runs [r0, r1); their descriptors are fetched once, one per lane (64 at a
-    // time), and broadcast with readlane, so no run waits on a dependent scalar load
-    const uint2* tb = tiles + (uint64_t)b * (P + 1);
-    const uint4* src = reinterpret_cast<const uint4*>(stage);
-    uint4* dst = reinterpret_cast<uint4*>(raw);
-    constexpr uint32_t NW = kBinSB / 64;
-    const uint32_t r0 = w * P / NW, r1 = (w + 1) * P / NW;
+    const uint4* s16 = reinterpret_cast<const uint4*>(src);
+    uint4* d16 = reinterpret_cast<uint4*>(dst);
     for (uint32_t g = r0; g < r1; g += 64) {
         const uint32_t ng = r1 - g < 64 ? r1 - g : 64;
         uint2 dsc = make_uint2(0u, 0u);
@@ -122,13 +79,90 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
         for (uint32_t k = 0; k < ng; ++k) {
             const uint32_t so = __builtin_amdgcn_readlane(dsc.x, k);
             const uint32_t pre = __builtin_amdgcn_readlane(dsc.y, k);
-            const uint32_t n16 = (__builtin_amdgcn_readlane(nxt, k) - pre) >> 1;   // 16-byte units (padded run)
-            const uint4* sp = src + (so >> 1) + lane;
-            uint4* dp = dst + (pre >> 1);
+            const uint32_t n16 = (__builtin_amdgcn_readlane(nxt, k) - pre) >> 1;   // 16-byte units
+            const uint4* sp = s16 + (so >> 1) + lane;
+            uint4* dp = d16 + (pre >> 1);
             for (uint32_t o = 0; o < n16; o += 64)
                 if (o + lane < n16) __builtin_amdgcn_global_load_lds(sp + o, dp + o, 16, 0, 0);
         }
     }
+}
+
+// ------------------------------------------------------------------------------ phase A
+__global__ __launch_bounds__(kBinA) void k_bin_scatter(const double* __restrict__ x, const uint16_t* __restrict__ idxA,
+                                                     const uint64_t* __restrict__ aoff, double* __restrict__ stage,
+                                                     const InstState* __restrict__ st, uint64_t N, uint32_t SA,
+                                                     uint32_t segs, uint32_t chunk) {
+    extern __shared__ double lx[];
+    if (st->done) return;
+    const uint32_t a = blockIdx.x / segs, sg = blockIdx.x % segs;
+    const uint64_t pa1 = aoff[a + 1];
+    const uint64_t p0 = aoff[a] + (uint64_t)sg * chunk;
+    if (p0 >= pa1) return;
+    const uint64_t p1 = p0 + chunk < pa1 ? p0 + chunk : pa1;
+    const uint64_t base = (uint64_t)a * SA;
+    const uint32_t n = (uint32_t)(N - base < SA ? N - base : SA);
+    {   // x block -> LDS by LDS-DMA, 16 B per lane (x is allocated with spare elements, so the
+        // last odd element's pair never reads past the buffer)
+        const uint32_t n16 = (n + 1) / 2;
+        const uint4* xs = reinterpret_cast<const uint4*>(x + base) + threadIdx.x;
+        uint4* ld = reinterpret_cast<uint4*>(lx) + (threadIdx.x & ~63u);
+        for (uint32_t o = 0; o < n16; o += kBinA)
+            if (o + threadIdx.x < n16) __builtin_amdgcn_global_load_lds(xs + o, ld + o, 16, 0, 0);
+    }
+    __syncthreads();
+    bin_stream(lx, idxA, stage, p0, p1);
+}
+
+// ------------------------------------------------------------------------------ phase M
+// mt[g][0..PK] (g = r*K + k): (stage1 start, image offset) of run (a = k*PK + j, r); entry PK holds
+// the image size.  moff[g] .. moff[g+1]: the group's output range in stage2.
+__global__ __launch_bounds__(kBinA) void k_bin_regroup(const double* __restrict__ stage1, const uint2* __restrict__ mt,
+                                                     const uint64_t* __restrict__ moff, const uint16_t* __restrict__ idxM,
+                                                     double* __restrict__ stage2, const InstState* __restrict__ st,
+                                                     uint32_t PK) {
+    extern __shared__ double lm[];
+    if (st->done) return;
+    const uint32_t g = blockIdx.x;
+    constexpr uint32_t NW = kBinA / 64;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    bin_dma_runs(mt + (uint64_t)g * (PK + 1), w * PK / NW, (w + 1) * PK / NW, stage1, lm);
+    __syncthreads();
+    bin_stream(lm, idxM, stage2, moff[g], moff[g + 1]);
+}
+
+// ------------------------------------------------------------------------------ phase B
+// The runs of block b (run j of a table row of nrun + 1 descriptors) are copied into LDS,
+// concatenated; lane i_local then reads its D values at invpos[b][t][i_local].
+template <int D, int T>
+__global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const double* __restrict__ stage,
+                                                       const uint16_t* __restrict__ invpos,
+                                                       const uint2* __restrict__ tiles, uint32_t nrun, uint32_t Q,
+                                                       uint32_t Qc) {
+    static_assert(D % 8 == 0, "invpos is read 8 slots at a time");
+    // runs are padded to even lengths; nrun <= D*kBinSB/16 (checked when the plan is built)
+    __shared__ __attribute__((aligned(16))) double raw[D * kBinSB + D * kBinSB / 16];
+    InstState* S = a.st;
+    if (S->done) return;
+    // XCD-aware order: consecutive receiver blocks (which share the lines at their tile-run
+    // seams) run on the same XCD (dispatch is round-robin over the 8 XCDs by blockIdx)
+    const uint32_t b = (blockIdx.x & 7u) * Qc + (blockIdx.x >> 3);
+    if (b >= Q) {   // partial slots past this partition's blocks: neutral (the finalize folds a.nblk)
+        if (b < a.nblk && threadIdx.x == 0) a.partial[b] = make_double2(kInf, -kInf);
+        return;
+    }
+    constexpr uint32_t NW = kBinSB / 64;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t li = (uint64_t)b * kBinSB + threadIdx.x;   // local row
+    const uint64_t i = a.row0 + li;                              // global receiver
+    const bool live = li < a.nrows;
+    // ordinary loads first (their wait is the barrier's vmcnt(0) anyway)
+    const double xi = live ? a.xin[i] : 0.0;
+    uint4 ip[D / 8];
+    const uint4* ipp = reinterpret_cast<const uint4*>(invpos) + (uint64_t)b * (D / 8) * kBinSB + threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < D / 8; ++q) ip[q] = ipp[q * kBinSB];
+    bin_dma_runs(tiles + (uint64_t)b * (nrun + 1), w * nrun / NW, (w + 1) * nrun / NW, stage, raw);
     __syncthreads();
 
     double mn = kInf, mx = -kInf;
@@ -153,23 +187,38 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
 }
 
 // ------------------------------------------------------------------------------ plan build
+// Geometry shared by the setup kernels.  Local receiver rows li in [0, NR) (a node partition's
+// rows, or all N); global sender ids j in [0, N).
+//   one level:  key1 = a*Q + b                         (phase B reads stage1)
+//   two levels: key1 = a*R + r, key2 = (r*K + k)*QR + bl  with r = li / SR, k = a / PK,
+//               bl = (li % SR) / kBinSB                (phase B reads stage2)
+struct BinGeom {
+    uint32_t D, dp, SA, P, Q, levels, SR, R, K, PK, QR;
+};
+
 __device__ __forceinline__ uint32_t ell_at(const uint32_t* ell, uint64_t i, uint32_t t, uint32_t dp) {
     return ell[(((i >> 6) * (dp >> 2) + (t >> 2)) * 64 + (i & 63)) * 4 + (t & 3)];
 }
 
-__global__ __launch_bounds__(256) void k_bin_keys(const uint32_t* __restrict__ ell, uint64_t E, uint32_t D,
-                                                  uint32_t dp, uint32_t SA, uint32_t Q, uint32_t* __restrict__ keys,
-                                                  uint32_t* __restrict__ vals) {
+__global__ __launch_bounds__(256) void k_bin_keys(const uint32_t* __restrict__ ell, uint64_t E, BinGeom G, int level,
+                                                  uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
     const uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (e >= E) return;
-    const uint64_t i = e / D;
-    const uint32_t t = (uint32_t)(e % D);
-    const uint32_t j = ell_at(ell, i, t, dp);
-    keys[e] = (j / SA) * Q + (uint32_t)(i / kBinSB);
+    const uint64_t li = e / G.D;
+    const uint32_t t = (uint32_t)(e % G.D);
+    const uint32_t a = ell_at(ell, li, t, G.dp) / G.SA;
+    uint32_t key;
+    if (G.levels == 1)
+        key = a * G.Q + (uint32_t)(li / kBinSB);
+    else if (level == 1)
+        key = a * G.R + (uint32_t)(li / G.SR);
+    else
+        key = ((uint32_t)(li / G.SR) * G.K + a / G.PK) * G.QR + (uint32_t)((li % G.SR) / kBinSB);
+    keys[e] = key;
     vals[e] = (uint32_t)e;
 }
 
-// tile boundaries in the sorted keys: tl[key] = (first, last+1) unpadded A-order positions
+// tile boundaries in the sorted keys: tl[key] = (first, last+1) unpadded sorted positions
 __global__ __launch_bounds__(256) void k_bin_bounds(uint64_t E, const uint32_t* __restrict__ ks, uint2* __restrict__ tl) {
     const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (p >= E) return;
@@ -178,7 +227,7 @@ __global__ __launch_bounds__(256) void k_bin_bounds(uint64_t E, const uint32_t* 
     if (p == E - 1 || ks[p + 1] != key) tl[key].y = (uint32_t)(p + 1);
 }
 
-// padded tile lengths (even, so every run starts 16-byte aligned in stage and in LDS)
+// padded tile lengths (even, so every run starts 16-byte aligned in the stage and in LDS)
 __global__ __launch_bounds__(256) void k_bin_plen(const uint2* __restrict__ tl, uint64_t nt, uint32_t* __restrict__ plen) {
     const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (k >= nt) return;
@@ -186,62 +235,111 @@ __global__ __launch_bounds__(256) void k_bin_plen(const uint2* __restrict__ tl, 
     plen[k] = t.y ? (t.y - t.x + 1u) & ~1u : 0u;
 }
 
-__global__ __launch_bounds__(256) void k_bin_fill(const uint32_t* __restrict__ ell, uint64_t E, uint32_t D,
-                                                  uint32_t dp, uint32_t SA, const uint32_t* __restrict__ ks,
-                                                  const uint32_t* __restrict__ vs, const uint2* __restrict__ tl,
-                                                  const uint32_t* __restrict__ pstart, uint16_t* __restrict__ idxA) {
+// idxA[padded position] = sender index inside its source block (level-1 order)
+__global__ __launch_bounds__(256) void k_bin_fill_a(const uint32_t* __restrict__ ell, uint64_t E, BinGeom G,
+                                                    const uint32_t* __restrict__ ks, const uint32_t* __restrict__ vs,
+                                                    const uint2* __restrict__ tl, const uint32_t* __restrict__ pstart,
+                                                    uint16_t* __restrict__ idxA) {
     const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (p >= E) return;
     const uint32_t e = vs[p], key = ks[p];
-    const uint64_t i = e / D;
-    const uint32_t t = e % D;
-    idxA[pstart[key] + (p - tl[key].x)] = (uint16_t)(ell_at(ell, i, t, dp) % SA);
+    idxA[pstart[key] + (p - tl[key].x)] = (uint16_t)(ell_at(ell, e / G.D, e % G.D, G.dp) % G.SA);
 }
 
-// per receiver block b: tiles[b][a] = (padded A-order start, element offset of run a inside the
-// block's concatenated padded runs), tiles[b][P] = (0, total)
-__global__ __launch_bounds__(256) void k_bin_prefix(const uint32_t* __restrict__ pstart, const uint32_t* __restrict__ plen,
-                                                    uint2* __restrict__ tiles, uint32_t P, uint32_t Q) {
-    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
-    if (b >= Q) return;
+// phase-A ranges: aoff[a] = padded start of source block a's deliveries (aoff[P] = Ep)
+__global__ __launch_bounds__(256) void k_bin_aoff(const uint32_t* __restrict__ pstart, uint32_t P, uint32_t G1,
+                                                  uint64_t Ep, uint64_t* __restrict__ aoff) {
+    const uint32_t a = blockIdx.x * 256 + threadIdx.x;
+    if (a > P) return;
+    aoff[a] = a < P ? pstart[(uint64_t)a * G1] : Ep;
+}
+
+// phase-M run tables: mt[g][j] for group g = r*K + k, run a = k*PK + j; total image size in cap[g]
+__global__ __launch_bounds__(256) void k_bin_mtiles(const uint32_t* __restrict__ pstart1, const uint32_t* __restrict__ plen1,
+                                                    BinGeom G, uint2* __restrict__ mt, uint32_t* __restrict__ cap) {
+    const uint32_t g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= G.R * G.K) return;
+    const uint32_t r = g / G.K, k = g % G.K;
     uint32_t pre = 0;
-    for (uint32_t a = 0; a < P; ++a) {
-        const uint64_t key = (uint64_t)a * Q + b;
-        tiles[(uint64_t)b * (P + 1) + a] = make_uint2(pstart[key], pre);
+    for (uint32_t j = 0; j < G.PK; ++j) {
+        const uint32_t a = k * G.PK + j;
+        if (a < G.P) {
+            const uint64_t key = (uint64_t)a * G.R + r;
+            mt[(uint64_t)g * (G.PK + 1) + j] = make_uint2(pstart1[key], pre);
+            pre += plen1[key];
+        } else {
+            mt[(uint64_t)g * (G.PK + 1) + j] = make_uint2(0u, pre);
+        }
+    }
+    mt[(uint64_t)g * (G.PK + 1) + G.PK] = make_uint2(0u, pre);
+    cap[g] = pre;
+}
+
+// lpos[e] = position of delivery e inside its phase-M LDS image
+__global__ __launch_bounds__(256) void k_bin_lpos(uint64_t E, BinGeom G, const uint32_t* __restrict__ ks1,
+                                                  const uint32_t* __restrict__ vs1, const uint2* __restrict__ tl1,
+                                                  const uint2* __restrict__ mt, uint16_t* __restrict__ lpos) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= E) return;
+    const uint32_t key = ks1[p], a = key / G.R, r = key % G.R;
+    const uint32_t g = r * G.K + a / G.PK;
+    lpos[vs1[p]] = (uint16_t)(mt[(uint64_t)g * (G.PK + 1) + a % G.PK].y + (p - tl1[key].x));
+}
+
+// idxM[padded level-2 position] = lpos of that delivery
+__global__ __launch_bounds__(256) void k_bin_fill_m(uint64_t E, const uint32_t* __restrict__ ks2,
+                                                    const uint32_t* __restrict__ vs2, const uint2* __restrict__ tl2,
+                                                    const uint32_t* __restrict__ pstart2, const uint16_t* __restrict__ lpos,
+                                                    uint16_t* __restrict__ idxM) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= E) return;
+    const uint32_t key = ks2[p];
+    idxM[pstart2[key] + (p - tl2[key].x)] = lpos[vs2[p]];
+}
+
+// phase-M output ranges: moff[g] = padded level-2 start of group g (moff[R*K] = Ep2)
+__global__ __launch_bounds__(256) void k_bin_moff(const uint32_t* __restrict__ pstart2, BinGeom G, uint64_t Ep2,
+                                                  uint64_t* __restrict__ moff) {
+    const uint32_t g = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t ng = G.R * G.K;
+    if (g > ng) return;
+    moff[g] = g < ng ? pstart2[(uint64_t)g * G.QR] : Ep2;
+}
+
+// Runs read by phase B for block b: one level: keys j*Q + b (j = source block, nrun = P); two
+// levels: keys (r*K + j)*QR + bl (j = chunk, nrun = K).
+__device__ __forceinline__ uint64_t bin_run_key(const BinGeom& G, uint32_t b, uint32_t j) {
+    if (G.levels == 1) return (uint64_t)j * G.Q + b;
+    return ((uint64_t)(b / G.QR) * G.K + j) * G.QR + b % G.QR;
+}
+
+// tiles[b][j] = (padded start, element offset inside block b's concatenated runs); tiles[b][nrun] = (0, total)
+__global__ __launch_bounds__(256) void k_bin_prefix(const uint32_t* __restrict__ pstart, const uint32_t* __restrict__ plen,
+                                                    BinGeom G, uint32_t nrun, uint2* __restrict__ tiles) {
+    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= G.Q) return;
+    uint32_t pre = 0;
+    for (uint32_t j = 0; j < nrun; ++j) {
+        const uint64_t key = bin_run_key(G, b, j);
+        tiles[(uint64_t)b * (nrun + 1) + j] = make_uint2(pstart[key], pre);
         pre += plen[key];
     }
-    tiles[(uint64_t)b * (P + 1) + P] = make_uint2(0u, pre);
+    tiles[(uint64_t)b * (nrun + 1) + nrun] = make_uint2(0u, pre);
 }
 
 // invpos[b][t/8][i_local][t%8] = element position of (receiver i_local, slot t) in block b's runs
-__global__ __launch_bounds__(256) void k_bin_inv(uint64_t E, uint32_t D, uint32_t P, uint32_t Q,
-                                                 const uint32_t* __restrict__ ks, const uint32_t* __restrict__ vs,
-                                                 const uint2* __restrict__ tl, const uint2* __restrict__ tiles,
-                                                 uint16_t* __restrict__ invpos) {
+__global__ __launch_bounds__(256) void k_bin_inv(uint64_t E, BinGeom G, uint32_t nrun, const uint32_t* __restrict__ ks,
+                                                 const uint32_t* __restrict__ vs, const uint2* __restrict__ tl,
+                                                 const uint2* __restrict__ tiles, uint16_t* __restrict__ invpos) {
     const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (p >= E) return;
-    const uint32_t e = vs[p];
-    const uint64_t i = e / D;
-    const uint32_t t = e % D;
-    const uint32_t key = ks[p], a = key / Q, b = key % Q;
-    const uint32_t pos = tiles[(uint64_t)b * (P + 1) + a].y + (uint32_t)(p - tl[key].x);
-    const uint32_t il = (uint32_t)(i % kBinSB);
-    invpos[(((uint64_t)b * (D / 8) + t / 8) * kBinSB + il) * 8 + (t & 7)] = (uint16_t)pos;
-}
-
-// aoffc[a][c] = padded A-order start of tile (a, first receiver block of chunk c)
-__global__ __launch_bounds__(256) void k_bin_aoffc(const uint32_t* __restrict__ pstart, uint32_t P, uint32_t Q,
-                                                   uint32_t C, uint64_t Ep, uint64_t* __restrict__ aoffc) {
-    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-    if (k >= P * (C + 1)) return;
-    const uint32_t a = k / (C + 1), c = k % (C + 1);
-    const uint64_t key = (uint64_t)a * Q + (uint64_t)c * Q / C;
-    aoffc[k] = key < (uint64_t)P * Q ? pstart[key] : Ep;
-}
-
-__global__ __launch_bounds__(256) void k_fill_u64(uint64_t* p, uint64_t n, uint64_t v) {
-    const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (k < n) p[k] = v;
+    const uint32_t e = vs[p], key = ks[p];
+    const uint64_t li = e / G.D;
+    const uint32_t t = e % G.D;
+    const uint32_t b = (uint32_t)(li / kBinSB);
+    const uint32_t j = G.levels == 1 ? key / G.Q : (key / G.QR) % G.K;
+    const uint32_t pos = tiles[(uint64_t)b * (nrun + 1) + j].y + (uint32_t)(p - tl[key].x);
+    invpos[(((uint64_t)b * (G.D / 8) + t / 8) * kBinSB + (li % kBinSB)) * 8 + (t & 7)] = (uint16_t)pos;
 }
 
 // ------------------------------------------------------------------------------ host side
@@ -256,44 +354,60 @@ bool binned_supported(uint32_t d, uint32_t t, uint32_t rule) {
     return false;
 }
 
+uint32_t binned_levels(uint64_t N, uint64_t NR, uint32_t d, uint32_t sa, uint32_t* sr_out) {
+    if (d == 0 || sa == 0 || NR == 0) return 0;
+    const uint64_t P = (N + sa - 1) / sa;
+    const uint64_t Q = (NR + kBinSB - 1) / kBinSB;
+    const double run1 = (double)NR * d / ((double)P * (double)Q);
+    if (run1 >= 64.0) {
+        if (sr_out) *sr_out = kBinSB;
+        return (uint64_t)P <= (uint64_t)d * kBinSB / 16 ? 1u : 0u;   // phase-B LDS bound
+    }
+    // level-1 runs (a, r) average NR*d / (P * R) with R = NR / SR: about 128 at SR = 128 * P / d
+    uint64_t sr = (128ull * P / d + kBinSB - 1) / kBinSB * kBinSB;
+    if (sr < 4 * kBinSB) sr = 4 * kBinSB;
+    if (sr > 65536) return 0;
+    if (sr_out) *sr_out = (uint32_t)sr;
+    return 2;
+}
+
 void binned_free(BinnedPlan& p) {
     (void)hipFree(p.idxA);
+    (void)hipFree(p.idxM);
     (void)hipFree(p.invpos);
     (void)hipFree(p.tiles);
-    (void)hipFree(p.aoffc);
-    (void)hipFree(p.stage);
+    (void)hipFree(p.mt);
+    (void)hipFree(p.aoff);
+    (void)hipFree(p.moff);
+    (void)hipFree(p.stage1);
+    (void)hipFree(p.stage2);
     p = BinnedPlan{};
 }
 
-hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint32_t d, uint32_t dp, uint32_t sa,
-                        uint32_t chunks, hipStream_t s) {
-    hipError_t e;
-    p.D = d;
-    p.SA = sa;
-    p.E = N * d;
-    p.P = (uint32_t)((N + sa - 1) / sa);
-    p.Q = (uint32_t)((N + kBinSB - 1) / kBinSB);
-    p.C = chunks < 1 ? 1 : chunks > p.Q ? p.Q : chunks;
-    // deliveries per phase-A workgroup (a multiple of the 4096-position super-step): about 512
-    // workgroups per launch (two generations per CU measured faster than one), few x-block refills
-    {
-        const uint64_t per_a = ((uint64_t)sa * d + p.C - 1) / p.C;
-        const uint64_t want = (512 + p.P - 1) / p.P;
-        uint64_t ch = (per_a + want - 1) / want;
-        ch = ch < 8192 ? 8192 : ch;
-        p.chunk = (uint32_t)((ch + 4095) / 4096 * 4096);
-    }
-    p.segs = 1;   // set from the real per-(a, c) range lengths once aoffc is built
-    const uint64_t E = p.E, nt = (uint64_t)p.P * p.Q;
-    if (E >= (1ull << 31) || nt >= (1ull << 32)) return hipErrorNotSupported;
-    const uint64_t Qp = (uint64_t)p.Q * kBinSB;   // receiver slots incl. the ragged last block's padding
-    if ((e = hipMalloc(&p.invpos, Qp * d * 2)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(p.invpos, 0, Qp * d * 2, s)) != hipSuccess) return e;
-    if ((e = hipMalloc(&p.tiles, ((uint64_t)p.P + 1) * p.Q * sizeof(uint2))) != hipSuccess) return e;
-    if ((e = hipMalloc(&p.aoffc, (uint64_t)p.P * (p.C + 1) * sizeof(uint64_t))) != hipSuccess) return e;
+namespace {
 
-    uint32_t *keys = nullptr, *vals = nullptr, *ks = nullptr, *vs = nullptr, *plen = nullptr, *pstart = nullptr;
+// Deliveries sorted by a tile key (stable LSD radix sort: ties stay in (row, slot) order) and the
+// tiles padded to even lengths.  Owns its arrays.
+struct TileSort {
+    uint32_t *ks = nullptr, *vs = nullptr, *plen = nullptr, *pstart = nullptr;
     uint2* tl = nullptr;
+    uint64_t nt = 0, Ep = 0;
+    void release() {
+        (void)hipFree(ks);
+        (void)hipFree(vs);
+        (void)hipFree(plen);
+        (void)hipFree(pstart);
+        (void)hipFree(tl);
+        ks = vs = plen = pstart = nullptr;
+        tl = nullptr;
+    }
+};
+
+hipError_t tile_sort(const uint32_t* ell, uint64_t E, const BinGeom& G, int level, uint64_t nt, TileSort& T,
+                     hipStream_t s) {
+    hipError_t e;
+    T.nt = nt;
+    uint32_t *keys = nullptr, *vals = nullptr;
     void* temp = nullptr;
     size_t tb = 0, tb2 = 0;
     int bits = 1;
@@ -301,98 +415,200 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint32_t
     const unsigned grid = (unsigned)((E + 255) / 256), gridt = (unsigned)((nt + 255) / 256);
     e = hipMalloc(&keys, E * 4);
     if (e == hipSuccess) e = hipMalloc(&vals, E * 4);
-    if (e == hipSuccess) e = hipMalloc(&ks, E * 4);
-    if (e == hipSuccess) e = hipMalloc(&vs, E * 4);
-    if (e == hipSuccess) e = hipMalloc(&tl, nt * sizeof(uint2));
-    if (e == hipSuccess) e = hipMalloc(&plen, nt * 4);
-    if (e == hipSuccess) e = hipMalloc(&pstart, nt * 4);
-    if (e == hipSuccess) e = hipMemsetAsync(tl, 0, nt * sizeof(uint2), s);
+    if (e == hipSuccess) e = hipMalloc(&T.ks, E * 4);
+    if (e == hipSuccess) e = hipMalloc(&T.vs, E * 4);
+    if (e == hipSuccess) e = hipMalloc(&T.tl, nt * sizeof(uint2));
+    if (e == hipSuccess) e = hipMalloc(&T.plen, nt * 4);
+    if (e == hipSuccess) e = hipMalloc(&T.pstart, nt * 4);
+    if (e == hipSuccess) e = hipMemsetAsync(T.tl, 0, nt * sizeof(uint2), s);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_bin_keys, dim3(grid), dim3(256), 0, s, ell, E, d, dp, sa, p.Q, keys, vals);
+        hipLaunchKernelGGL(k_bin_keys, dim3(grid), dim3(256), 0, s, ell, E, G, level, keys, vals);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, ks, vals, vs, (int)E, 0, bits, s);
-    if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, plen, pstart, (int)nt, s);
+    if (e == hipSuccess) e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, T.ks, vals, T.vs, (int)E, 0, bits, s);
+    if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, T.plen, T.pstart, (int)nt, s);
     if (tb2 > tb) tb = tb2;
     if (e == hipSuccess) e = hipMalloc(&temp, tb ? tb : 16);
-    if (e == hipSuccess)   // LSD radix sort is stable: (a, b, then i, slot) order
-        e = hipcub::DeviceRadixSort::SortPairs(temp, tb, keys, ks, vals, vs, (int)E, 0, bits, s);
+    if (e == hipSuccess) e = hipcub::DeviceRadixSort::SortPairs(temp, tb, keys, T.ks, vals, T.vs, (int)E, 0, bits, s);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_bin_bounds, dim3(grid), dim3(256), 0, s, E, ks, tl);
-        hipLaunchKernelGGL(k_bin_plen, dim3(gridt), dim3(256), 0, s, tl, nt, plen);
+        hipLaunchKernelGGL(k_bin_bounds, dim3(grid), dim3(256), 0, s, E, T.ks, T.tl);
+        hipLaunchKernelGGL(k_bin_plen, dim3(gridt), dim3(256), 0, s, T.tl, nt, T.plen);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(temp, tb, plen, pstart, (int)nt, s);
+    if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(temp, tb, T.plen, T.pstart, (int)nt, s);
     uint32_t last[2] = {0, 0};
-    if (e == hipSuccess) e = hipMemcpyAsync(&last[0], pstart + nt - 1, 4, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(&last[1], plen + nt - 1, 4, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    p.Ep = (uint64_t)last[0] + last[1];
-    if (e == hipSuccess) e = hipMalloc(&p.idxA, p.Ep * 2);
-    if (e == hipSuccess) e = hipMemsetAsync(p.idxA, 0, p.Ep * 2, s);
-    if (e == hipSuccess) e = hipMalloc(&p.stage, p.Ep * sizeof(double));
+    if (e == hipSuccess) e = hipMemcpyAsync(&last[0], T.pstart + nt - 1, 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(&last[1], T.plen + nt - 1, 4, hipMemcpyDeviceToHost, s);
+    hipError_t e2 = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = e2;
+    T.Ep = (uint64_t)last[0] + last[1];
+    (void)hipFree(temp);
+    (void)hipFree(keys);
+    (void)hipFree(vals);
+    return e;
+}
+
+}  // namespace
+
+hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t NR, uint32_t d, uint32_t dp,
+                        uint32_t sa, hipStream_t s) {
+    hipError_t e = hipSuccess;
+    uint32_t sr = 0;
+    const uint32_t levels = binned_levels(N, NR, d, sa, &sr);
+    if (!levels) return hipErrorNotSupported;
+    BinGeom G{};
+    G.D = d;
+    G.dp = dp;
+    G.SA = sa;
+    G.P = (uint32_t)((N + sa - 1) / sa);
+    G.Q = (uint32_t)((NR + kBinSB - 1) / kBinSB);
+    G.levels = levels;
+    G.SR = sr;
+    G.R = levels == 1 ? G.Q : (uint32_t)((NR + sr - 1) / sr);
+    G.QR = sr / kBinSB;
+    G.PK = 1;
+    if (levels == 2) {   // chunks of PK source blocks: an LDS image of about 16 Ki deliveries
+        const double run1 = (double)NR * d / ((double)G.P * G.R);
+        const uint32_t pk = (uint32_t)(16384.0 / run1);
+        G.PK = pk < 1 ? 1 : pk > G.P ? G.P : pk;
+    }
+    G.K = (G.P + G.PK - 1) / G.PK;
+    p.D = d;
+    p.SA = sa;
+    p.P = G.P;
+    p.Q = G.Q;
+    p.levels = levels;
+    p.E = NR * d;
+    p.PK = G.PK;
+    p.ngroups = levels == 2 ? G.R * G.K : 0;
+    p.nrun = levels == 1 ? G.P : G.K;
+    const uint64_t E = p.E;
+    const uint64_t nt1 = (uint64_t)G.P * G.R;
+    const uint64_t nt2 = levels == 2 ? (uint64_t)G.R * G.K * G.QR : 0;
+    if (E >= (1ull << 32) || nt1 >= (1ull << 32) || nt2 >= (1ull << 32)) return hipErrorNotSupported;
+    if ((uint64_t)p.nrun > (uint64_t)d * kBinSB / 16) return hipErrorNotSupported;   // phase-B LDS bound
+    const unsigned grid = (unsigned)((E + 255) / 256);
+
+    // ---- level 1 (phase A): key (a, b) or (a, r)
+    TileSort T1, T2;
+    e = tile_sort(ell, E, G, 1, nt1, T1, s);
+    p.Ep1 = T1.Ep;
+    if (e == hipSuccess) e = hipMalloc(&p.idxA, p.Ep1 * 2);
+    if (e == hipSuccess) e = hipMemsetAsync(p.idxA, 0, p.Ep1 * 2, s);
+    if (e == hipSuccess) e = hipMalloc(&p.stage1, p.Ep1 * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc(&p.aoff, ((uint64_t)G.P + 1) * sizeof(uint64_t));
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_bin_fill, dim3(grid), dim3(256), 0, s, ell, E, d, dp, sa, ks, vs, tl, pstart, p.idxA);
-        hipLaunchKernelGGL(k_bin_prefix, dim3((p.Q + 255) / 256), dim3(256), 0, s, pstart, plen, p.tiles, p.P, p.Q);
-        hipLaunchKernelGGL(k_bin_inv, dim3(grid), dim3(256), 0, s, E, d, p.P, p.Q, ks, vs, tl, p.tiles, p.invpos);
-        const uint32_t n = p.P * (p.C + 1);
-        hipLaunchKernelGGL(k_bin_aoffc, dim3((n + 255) / 256), dim3(256), 0, s, pstart, p.P, p.Q, p.C, p.Ep, p.aoffc);
+        hipLaunchKernelGGL(k_bin_fill_a, dim3(grid), dim3(256), 0, s, ell, E, G, T1.ks, T1.vs, T1.tl, T1.pstart, p.idxA);
+        hipLaunchKernelGGL(k_bin_aoff, dim3((G.P + 256) / 256), dim3(256), 0, s, T1.pstart, G.P, G.R, p.Ep1, p.aoff);
+        e = hipGetLastError();
+    }
+    TileSort* last = &T1;
+    if (e == hipSuccess && levels == 2) {
+        // ---- level 2 (phase M): PK-run images per (r, k), regrouped by receiver block
+        uint16_t* lpos = nullptr;
+        uint32_t* cap = nullptr;
+        const uint32_t ng = p.ngroups;
+        e = hipMalloc(&p.mt, (uint64_t)ng * (G.PK + 1) * sizeof(uint2));
+        if (e == hipSuccess) e = hipMalloc(&cap, (uint64_t)ng * 4);
+        if (e == hipSuccess) e = hipMalloc(&lpos, E * 2);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_bin_mtiles, dim3((ng + 255) / 256), dim3(256), 0, s, T1.pstart, T1.plen, G, p.mt, cap);
+            hipLaunchKernelGGL(k_bin_lpos, dim3(grid), dim3(256), 0, s, E, G, T1.ks, T1.vs, T1.tl, p.mt, lpos);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) {   // every image must fit the phase-M LDS
+            std::vector<uint32_t> h(ng);
+            e = hipMemcpyAsync(h.data(), cap, (uint64_t)ng * 4, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            uint32_t mx = 0;
+            for (uint32_t v : h) mx = v > mx ? v : mx;
+            p.mcap = mx;
+            if (e == hipSuccess && mx > kBinMCap) e = hipErrorNotSupported;
+        }
+        if (e == hipSuccess) e = tile_sort(ell, E, G, 2, nt2, T2, s);
+        p.Ep2 = T2.Ep;
+        if (e == hipSuccess) e = hipMalloc(&p.idxM, p.Ep2 * 2);
+        if (e == hipSuccess) e = hipMemsetAsync(p.idxM, 0, p.Ep2 * 2, s);
+        if (e == hipSuccess) e = hipMalloc(&p.stage2, p.Ep2 * sizeof(double));
+        if (e == hipSuccess) e = hipMalloc(&p.moff, ((uint64_t)ng + 1) * sizeof(uint64_t));
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_bin_fill_m, dim3(grid), dim3(256), 0, s, E, T2.ks, T2.vs, T2.tl, T2.pstart, lpos, p.idxM);
+            hipLaunchKernelGGL(k_bin_moff, dim3((ng + 256) / 256), dim3(256), 0, s, T2.pstart, G, p.Ep2, p.moff);
+            e = hipGetLastError();
+        }
+        hipError_t e2 = hipStreamSynchronize(s);
+        if (e == hipSuccess) e = e2;
+        (void)hipFree(lpos);
+        (void)hipFree(cap);
+        last = &T2;
+    }
+    // ---- phase B tables over the last stage
+    const uint64_t Qp = (uint64_t)G.Q * kBinSB;   // receiver slots incl. the ragged last block's padding
+    if (e == hipSuccess) e = hipMalloc(&p.invpos, Qp * d * 2);
+    if (e == hipSuccess) e = hipMemsetAsync(p.invpos, 0, Qp * d * 2, s);
+    if (e == hipSuccess) e = hipMalloc(&p.tiles, ((uint64_t)p.nrun + 1) * G.Q * sizeof(uint2));
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_bin_prefix, dim3((G.Q + 255) / 256), dim3(256), 0, s, last->pstart, last->plen, G, p.nrun,
+                           p.tiles);
+        hipLaunchKernelGGL(k_bin_inv, dim3(grid), dim3(256), 0, s, E, G, p.nrun, last->ks, last->vs, last->tl, p.tiles,
+                           p.invpos);
         e = hipGetLastError();
     }
     hipError_t e2 = hipStreamSynchronize(s);
     if (e == hipSuccess) e = e2;
-    if (e == hipSuccess) {   // every (a, c) range must be covered by segs workgroups of `chunk`
-        std::vector<uint64_t> h((uint64_t)p.P * (p.C + 1));
-        e = hipMemcpy(h.data(), p.aoffc, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost);
+    // phase-A segmentation: about 512 workgroups per launch (two generations per CU measured
+    // faster than one), a multiple of the 4096-position super-step, covering the longest block
+    if (e == hipSuccess) {
+        std::vector<uint64_t> h((uint64_t)G.P + 1);
+        e = hipMemcpy(h.data(), p.aoff, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost);
         uint64_t mx = 0;
-        for (uint32_t a = 0; a < p.P; ++a)
-            for (uint32_t c = 0; c < p.C; ++c) {
-                const uint64_t len = h[(uint64_t)a * (p.C + 1) + c + 1] - h[(uint64_t)a * (p.C + 1) + c];
-                if (len > mx) mx = len;
-            }
+        for (uint32_t a = 0; a < G.P; ++a) mx = h[a + 1] - h[a] > mx ? h[a + 1] - h[a] : mx;
+        const uint64_t want = (512 + G.P - 1) / G.P;
+        uint64_t ch = (mx + want - 1) / want;
+        ch = ch < 8192 ? 8192 : ch;
+        p.chunk = (uint32_t)((ch + 4095) / 4096 * 4096);
         p.segs = (uint32_t)((mx + p.chunk - 1) / p.chunk);
         if (p.segs == 0) p.segs = 1;
     }
-    (void)hipFree(temp);
-    (void)hipFree(keys);
-    (void)hipFree(vals);
-    (void)hipFree(ks);
-    (void)hipFree(vs);
-    (void)hipFree(tl);
-    (void)hipFree(plen);
-    (void)hipFree(pstart);
+    T1.release();
+    T2.release();
     return e;
 }
 
 hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, hipStream_t s) {
-    static bool attr = false;   // source blocks above 8192 senders need more than 64 KiB of LDS
+    static bool attr = false;   // source blocks above 8192 senders / phase-M images need > 64 KiB of LDS
     if (!attr) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_scatter),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 16384 * sizeof(double));
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_regroup),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, kBinMCap * sizeof(double));
         if (e != hipSuccess) return e;
         attr = true;
     }
-    for (uint32_t c = 0; c < p.C; ++c) {
-        hipLaunchKernelGGL(k_bin_scatter, dim3(p.P * p.segs), dim3(kBinA), p.SA * sizeof(double), s, a.xin, p.idxA,
-                           p.aoffc, p.stage, a.st, a.N, p.SA, p.segs, p.chunk, p.C, c);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        const uint32_t b0 = (uint32_t)((uint64_t)c * p.Q / p.C), b1 = (uint32_t)((uint64_t)(c + 1) * p.Q / p.C);
-        const uint32_t Qc = (b1 - b0 + 7) / 8;
-        const dim3 grid(8 * Qc);
-        bool ok = false;
-#define X(DD, TT)                                                                                   \
-        if (!ok && p.D == DD && a.trim == TT) {                                                     \
-            hipLaunchKernelGGL((k_bin_gather<DD, TT>), grid, dim3(kBinSB), 0, s, a, p.stage, p.invpos, \
-                               p.tiles, p.P, b0, b1, Qc);                                           \
-            ok = true;                                                                              \
-        }
-        ACS_BINNED_VARIANTS(X)
-#undef X
-        if (!ok) return hipErrorNotSupported;
+    hipLaunchKernelGGL(k_bin_scatter, dim3(p.P * p.segs), dim3(kBinA), p.SA * sizeof(double), s, a.xin, p.idxA, p.aoff,
+                       p.stage1, a.st, a.N, p.SA, p.segs, p.chunk);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const double* last = p.stage1;
+    if (p.levels == 2) {
+        hipLaunchKernelGGL(k_bin_regroup, dim3(p.ngroups), dim3(kBinA), (p.mcap + 2) * sizeof(double), s, p.stage1,
+                           p.mt, p.moff, p.idxM, p.stage2, a.st, p.PK);
         if ((e = hipGetLastError()) != hipSuccess) return e;
+        last = p.stage2;
     }
-    return hipSuccess;
+    const uint32_t nslot = a.nblk > p.Q ? a.nblk : p.Q;
+    const uint32_t Qc = (nslot + 7) / 8;
+    const dim3 grid(8 * Qc);
+#define X(DD, TT)                                                                                        \
+    if (p.D == DD && a.trim == TT) {                                                                     \
+        hipLaunchKernelGGL((k_bin_gather<DD, TT>), grid, dim3(kBinSB), 0, s, a, last, p.invpos, p.tiles, \
+                           p.nrun, p.Q, Qc);                                                             \
+        return hipGetLastError();                                                                        \
+    }
+    ACS_BINNED_VARIANTS(X)
+#undef X
+    return hipErrorNotSupported;
 }
 
 }  // namespace acs

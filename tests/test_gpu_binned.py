@@ -4,7 +4,9 @@ The binned path serves clean RANDOM_REGULAR configs with a sort-based rule (TRIM
 DLPSW) on one instance.  Bar: bit-exact final values, spread traces and rounds (the rule depends
 only on the multiset of received values, so the slot a value lands in cannot change the result).
 ACSIM_BIN_SA shrinks the source block so that small graphs still span many blocks and ragged
-last blocks; ACSIM_BINNED=0 forces the per-lane kernel for the cross-check.
+last blocks, and (below a mean of 64 deliveries per (source block, receiver block) tile) take the
+two-level plan with the phase-M regroup; ACSIM_BINNED=0 forces the per-lane kernel for the
+cross-check.
 """
 import contextlib
 import os
@@ -46,10 +48,10 @@ def run_gpu(cfg):
 CASES = {
     "d32_t5_eps_n50000_sa1024": (Config(n_nodes=50000, topology="regular", degree=32, rule="trimmed",
                                         trim=5, eps=1e-9, max_rounds=100, seed=5, trace_spread=True), 1024),
-    "d32_t5_eps_n50000_sa1024_c3": (Config(n_nodes=50000, topology="regular", degree=32, rule="trimmed",
-                                           trim=5, eps=1e-9, max_rounds=100, seed=5, trace_spread=True), (1024, 3)),
-    "d16_t5_n70001_sa2048_c5": (Config(n_nodes=70001, topology="regular", degree=16, rule="trimmed", trim=5,
-                                       eps=1e-9, max_rounds=100, seed=21, trace_spread=True), (2048, 5)),
+    "two_level_d16_t5_n100000_sa256": (Config(n_nodes=100000, topology="regular", degree=16, rule="trimmed",
+                                              trim=5, eps=1e-9, max_rounds=100, seed=21, trace_spread=True), 256),
+    "two_level_d32_mid_n150001_sa512": (Config(n_nodes=150001, topology="regular", degree=32, rule="midpoint",
+                                               trim=5, eps=1e-10, max_rounds=200, seed=22, trace_spread=True), 512),
     "d16_t5_fixed_odd_sa512": (Config(n_nodes=30011, topology="regular", degree=16, rule="trimmed", trim=5,
                                       termination="fixed", max_rounds=25, seed=9, trace_spread=True), 512),
     "d8_t2_midpoint_sa256": (Config(n_nodes=12345, topology="regular", degree=8, rule="midpoint", trim=2,
@@ -65,10 +67,11 @@ CASES = {
 @pytest.mark.parametrize("name", list(CASES))
 def test_binned_matches_oracle_and_per_lane(oracle_mod, name):
     cfg, sa = CASES[name]
-    sa, chunks = sa if isinstance(sa, tuple) else (sa, 1)
-    with env(ACSIM_BIN_SA=sa, ACSIM_BIN_CHUNKS=chunks):
+    with env(ACSIM_BIN_SA=sa):
         kb, rb, xb, tb = run_gpu(cfg)
     assert kb.startswith("k_bin_scatter"), kb
+    if name.startswith("two_level"):
+        assert "k_bin_regroup" in kb, kb
     with env(ACSIM_BINNED=0):
         kr, rr, xr, tr = run_gpu(cfg)
     assert kr.startswith("k_round_regular"), kr
@@ -81,12 +84,10 @@ def test_binned_matches_oracle_and_per_lane(oracle_mod, name):
     assert np.array_equal(tb, to) and np.array_equal(tr, to)
 
 
-@pytest.mark.parametrize("chunks", [1, 4])
-def test_binned_full_cfg4_fixed_matches_per_lane(chunks):
+def test_binned_full_cfg4_fixed_matches_per_lane():
     """Full-size headline graph (N = 2^20): 30 FIXED rounds, binned vs per-lane bit for bit."""
     cfg = preset("cfg4", max_rounds=30, trace_spread=True)
-    with env(ACSIM_BIN_CHUNKS=chunks):
-        kb, rb, xb, tb = run_gpu(cfg)
+    kb, rb, xb, tb = run_gpu(cfg)
     assert kb.startswith("k_bin_scatter"), kb
     with env(ACSIM_BINNED=0):
         _, rr, xr, tr = run_gpu(cfg)
@@ -112,3 +113,33 @@ def test_binned_round_chunks_and_resume():
             g.set_state(7, mid[None, :])
             g.run()
             assert np.array_equal(bits(g.values(0)), ref)
+
+
+def test_two_level_full_cfg5_matches_per_lane():
+    """Full-size cfg5 graph (N = 2^26, d = 16): the two-level plan, 3 FIXED rounds, bit for bit
+    against the per-lane kernel (which the oracle pins at smaller sizes)."""
+    cfg = preset("cfg5", max_rounds=3, trace_spread=True)
+    kb, rb, xb, tb = run_gpu(cfg)
+    assert "k_bin_regroup" in kb, kb
+    with env(ACSIM_BINNED=0):
+        _, rr, xr, tr = run_gpu(cfg)
+    assert np.array_equal(rb, rr) and np.array_equal(tb, tr)
+    assert np.array_equal(xb, xr)
+
+
+@pytest.mark.parametrize("parts", [3, 8])
+def test_two_level_virtual_partitions(oracle_mod, parts):
+    """Node partitions (each with its own local-row plan) against the oracle."""
+    cfg = Config(n_nodes=100000, topology="regular", degree=16, rule="trimmed", trim=5, eps=1e-9,
+                 max_rounds=100, seed=23, trace_spread=True)
+    with env(ACSIM_BIN_SA=256):
+        with acsim.Simulator(cfg, partitions=parts) as p:
+            assert "k_bin_regroup" in p.kernel_name(), p.kernel_name()
+            p.run()
+            pr, px = p.rounds(), bits(p.values(0))
+            for q in range(parts):
+                assert np.array_equal(bits(p.partition_values(q)), px), f"copy {q} differs"
+    with oracle_mod.OracleSimulator(cfg, threads=8) as o:
+        o.run()
+        assert np.array_equal(o.rounds(), pr)
+        assert np.array_equal(bits(o.values(0)), px)
