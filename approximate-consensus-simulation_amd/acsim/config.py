@@ -116,6 +116,9 @@ PRESETS = {
     # configs[2]: 1e5 instances x 64 nodes, 20% loss, averaging [G=1, eps=1e-6]
     "cfg3": Config(n_nodes=64, n_instances=100000, topology="complete", rule="average",
                    loss_p=0.2, mask_group=1, eps=1e-6, max_rounds=1000),
+    # cfg3 with 16-instance groups sharing drop masks (§A.5 G = 16): the batched W·X MFMA variant
+    "cfg3_g16": Config(n_nodes=64, n_instances=100000, topology="complete", rule="average",
+                       loss_p=0.2, mask_group=16, eps=1e-6, max_rounds=1000),
     # configs[3]: N=2^20 random 32-regular, trimmed t=5 (headline); timed in FIXED R=100
     "cfg4": Config(n_nodes=1 << 20, topology="random_regular", degree=32, rule="trimmed_mean",
                    trim=5, eps=1e-6, max_rounds=100, termination="fixed"),

@@ -64,6 +64,7 @@ struct acs_sim {
     bool clean = true;
     bool ell_sorted = false;       // rows stored ascending (clean + order-independent rule)
     bool binned = false;           // PATH_REGULAR served by the binned exchange (round_binned.hip)
+    bool mfma = false;             // PATH_BATCHED served by the MFMA group kernel (batched_mfma.hip)
     BinnedPlan bin{};
     MsgParams mp{};
     double* x[2] = {nullptr, nullptr};
@@ -439,7 +440,10 @@ static int advance(acs_sim* s, uint32_t k) {
         hipEvent_t e1;
         int rc = timing_begin(s, &e1);
         if (rc) return rc;
-        HIP_TRY(launch_batched_small(a, s->B, k, s->stream));
+        if (s->mfma)
+            HIP_TRY(launch_batched_mfma(a, s->B, k, s->stream));
+        else
+            HIP_TRY(launch_batched_small(a, s->B, k, s->stream));
         if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
         HIP_TRY(hipMemcpyAsync(s->h_ndone, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(hipStreamSynchronize(s->stream));
@@ -566,6 +570,11 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     if (cfg->topology == ACS_TOPO_COMPLETE && s->N <= kBatchedMaxN) {
         s->path = PATH_BATCHED;
         s->kname = batched_small_name((uint32_t)s->N, cfg->rule, cfg->fault_model != ACS_FAULT_NONE);
+        const char* env = getenv("ACSIM_MFMA");
+        s->mfma = !(env && env[0] == '0') &&
+                  batched_mfma_supported((uint32_t)s->N, cfg->rule, cfg->fault_model != ACS_FAULT_NONE, cfg->mask_group,
+                                         cfg->instance_offset);
+        if (s->mfma) s->kname = "k_batched_mfma<v_mfma_f64_16x16x4>";
     } else if (cfg->topology == ACS_TOPO_COMPLETE && s->B == 1 && !partitioned &&
                dense_supported(cfg->fault_model, cfg->byz_strategy, cfg->rule, s->mp.thr, s->N)) {
         s->path = PATH_DENSE;

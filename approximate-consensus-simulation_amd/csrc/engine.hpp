@@ -156,6 +156,10 @@ hipError_t launch_round_dense(const DenseArgs& a, hipStream_t s);
 // Persistent batched kernel: COMPLETE topology with N <= 64, one wavefront per instance,
 // state in VGPRs across rounds.
 constexpr uint32_t kBatchedMaxN = 64;
+// MFMA variant (batched_mfma.hip): AVERAGE, no faults, 16-instance groups sharing drop masks
+// (mask_group % 16 == 0); one wavefront per group, Y = W·X by v_mfma_f64_16x16x4_f64 (≤ 1e-12).
+bool batched_mfma_supported(uint32_t N, uint32_t rule, bool faults, uint32_t mask_group, uint64_t inst_offset);
+hipError_t launch_batched_mfma(const BatchArgs& a, uint64_t B, uint32_t k, hipStream_t s);
 hipError_t launch_batched_small(const BatchArgs& a, uint64_t B, uint32_t k, hipStream_t s);
 const char* batched_small_name(uint32_t N, uint32_t rule, bool faults);
 

@@ -18,6 +18,7 @@ CASES = {
     "cfg1_avg": dict(),
     "cfg2": dict(),
     "cfg3": dict(),
+    "cfg3_g16": dict(),
     "cfg4": dict(max_rounds=100),
     "cfg4_eps": dict(),
     "cfg4_byz": dict(),
