@@ -65,6 +65,7 @@ struct acs_sim {
     bool ell_sorted = false;       // rows stored ascending (clean + order-independent rule)
     bool binned = false;           // PATH_REGULAR served by the binned exchange (round_binned.hip)
     bool mfma = false;             // PATH_BATCHED served by the MFMA group kernel (batched_mfma.hip)
+    bool dense_persist = false;    // PATH_DENSE served by the persistent LDS-resident kernel
     BinnedPlan bin{};
     MsgParams mp{};
     double* x[2] = {nullptr, nullptr};
@@ -168,6 +169,12 @@ static int validate(const acs_config* c) {
     if (c->trace_spread && c->n_instances * ((uint64_t)c->max_rounds + 1) > (1ull << 28))
         return fail(ACS_EINVAL, "spread trace too large (B*(max_rounds+1) > 2^28)");
     return ACS_OK;
+}
+
+// Tuning / cross-check switches: ACSIM_<NAME>=0 turns an optional fast path off.
+static bool env_off(const char* name) {
+    const char* v = getenv(name);
+    return v && v[0] == '0';
 }
 
 static uint32_t drop_threshold(double p) {
@@ -421,7 +428,7 @@ static int advance(acs_sim* s, uint32_t k) {
     const uint32_t cap = s->c.max_rounds > s->round ? s->c.max_rounds - s->round : 0;
     if (k > cap) k = cap;
     if (k == 0) return ACS_OK;
-    if (s->path == PATH_BATCHED) {
+    if (s->path == PATH_BATCHED || s->dense_persist) {
         BatchArgs a{};
         a.x0 = s->x[0];
         a.x1 = s->x[1];
@@ -440,7 +447,9 @@ static int advance(acs_sim* s, uint32_t k) {
         hipEvent_t e1;
         int rc = timing_begin(s, &e1);
         if (rc) return rc;
-        if (s->mfma)
+        if (s->dense_persist)
+            HIP_TRY(launch_dense_persist(a, s->B, k, s->stream));
+        else if (s->mfma)
             HIP_TRY(launch_batched_mfma(a, s->B, k, s->stream));
         else
             HIP_TRY(launch_batched_small(a, s->B, k, s->stream));
@@ -575,10 +584,12 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
                   batched_mfma_supported((uint32_t)s->N, cfg->rule, cfg->fault_model != ACS_FAULT_NONE, cfg->mask_group,
                                          cfg->instance_offset);
         if (s->mfma) s->kname = "k_batched_mfma<v_mfma_f64_16x16x4>";
-    } else if (cfg->topology == ACS_TOPO_COMPLETE && s->B == 1 && !partitioned &&
+    } else if (cfg->topology == ACS_TOPO_COMPLETE && !partitioned &&
+               (s->B == 1 || (s->N <= kDensePersistMaxN && !env_off("ACSIM_DENSE_PERSIST"))) &&
                dense_supported(cfg->fault_model, cfg->byz_strategy, cfg->rule, s->mp.thr, s->N)) {
         s->path = PATH_DENSE;
-        s->kname = "k_dense_sort+k_dense_recv";
+        s->dense_persist = s->N <= kDensePersistMaxN && !env_off("ACSIM_DENSE_PERSIST");
+        s->kname = s->dense_persist ? "k_dense_persist" : "k_dense_sort+k_dense_recv";
     } else if (cfg->topology == ACS_TOPO_RANDOM_REGULAR && regular_fast_supported(s->d, cfg->trim, cfg->rule)) {
         s->path = PATH_REGULAR;
         s->kname = regular_fast_name(s->d, cfg->trim, s->clean);

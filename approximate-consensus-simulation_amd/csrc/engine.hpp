@@ -152,6 +152,9 @@ struct DenseArgs {
 bool dense_supported(uint32_t fault_model, uint32_t byz, uint32_t rule, uint32_t thr, uint64_t N);
 uint32_t dense_nblk(uint64_t N);
 hipError_t launch_round_dense(const DenseArgs& a, hipStream_t s);
+// Persistent dense variant: one workgroup per instance, x in LDS, k rounds per launch (N <= 4096).
+constexpr uint32_t kDensePersistMaxN = 4096;
+hipError_t launch_dense_persist(const BatchArgs& a, uint64_t B, uint32_t k, hipStream_t s);
 
 // Persistent batched kernel: COMPLETE topology with N <= 64, one wavefront per instance,
 // state in VGPRs across rounds.

@@ -21,52 +21,16 @@ namespace acs {
 constexpr int kDenseSortBlock = 1024;
 constexpr int kDenseRecvBlock = 256;   // 4 receivers (wavefronts) per block
 
-__global__ __launch_bounds__(kDenseSortBlock) void k_dense_sort(const DenseArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double sh[];
-    InstState* S = a.st;
-    if (S->done) return;
-    const uint32_t N = a.N, P = a.P, r = a.r;
-    __shared__ uint32_t cnt[3];   // base, byz, silent
-    if (threadIdx.x < 3) cnt[threadIdx.x] = 0;
-    __syncthreads();
-    uint32_t nb = 0, nz = 0, ns = 0;
-    for (uint32_t j = threadIdx.x; j < P; j += kDenseSortBlock) {
-        double v = kInf;
-        if (j < N) {
-            const uint32_t st = a.status ? a.status[j] : kHonest;
-            if (st == kHonest || (st != kByz && r < st)) {
-                v = a.x[j];
-                ++nb;
-            } else if (st == kByz) {
-                ++nz;
-            } else if (r > st) {
-                ++ns;
-            }
-        }
-        sh[j] = v;
-    }
-    // wavefront sums first: 1024 LDS atomics on one address serialise
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        nb += __shfl_xor(nb, o, 64);
-        nz += __shfl_xor(nz, o, 64);
-        ns += __shfl_xor(ns, o, 64);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&cnt[0], nb);
-        atomicAdd(&cnt[1], nz);
-        atomicAdd(&cnt[2], ns);
-    }
-    __syncthreads();
-    // Bitonic network over P wires held in registers: thread t owns wires t + 1024e (e < E).
-    // Compare distance j < 64: partner in the same wavefront (shuffle, no barrier);
-    // 64 <= j < 1024: partner in another wavefront (LDS exchange, one barrier pair);
-    // j >= 1024: partner in the same thread (register swap).  55 stages at P = 1024, of which
-    // only 10 touch LDS.
-    constexpr int EMAX = kGenericMaxM / kDenseSortBlock;   // 8
+// Ascending bitonic sort of sh[0..P) (P a power of two, +inf padded) by a 1024-thread block.
+// Thread t owns wires t + 1024e (e < E = P/1024) in registers; on return v[e] holds wire
+// t + 1024e of the sorted sequence (sh is scratch).  Compare distance j < 64: partner in the same
+// wavefront (shuffle, no barrier); 64 <= j < 1024: partner in another wavefront (LDS exchange,
+// one barrier pair); j >= 1024: partner in the same thread (register swap).  55 stages at
+// P = 1024, of which only 10 touch LDS.
+template <int EMAX>
+__device__ __forceinline__ void dense_bitonic(double* sh, uint32_t P, double (&v)[EMAX]) {
     const uint32_t E = (P + kDenseSortBlock - 1) / kDenseSortBlock;
     const uint32_t tid = threadIdx.x;
-    double v[EMAX];
 #pragma unroll
     for (int e = 0; e < EMAX; ++e) {
         const uint32_t idx = tid + kDenseSortBlock * e;
@@ -117,6 +81,50 @@ __global__ __launch_bounds__(kDenseSortBlock) void k_dense_sort(const DenseArgs 
             }
         }
     }
+}
+
+__global__ __launch_bounds__(kDenseSortBlock) void k_dense_sort(const DenseArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double sh[];
+    InstState* S = a.st;
+    if (S->done) return;
+    const uint32_t N = a.N, P = a.P, r = a.r;
+    __shared__ uint32_t cnt[3];   // base, byz, silent
+    if (threadIdx.x < 3) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t nb = 0, nz = 0, ns = 0;
+    for (uint32_t j = threadIdx.x; j < P; j += kDenseSortBlock) {
+        double v = kInf;
+        if (j < N) {
+            const uint32_t st = a.status ? a.status[j] : kHonest;
+            if (st == kHonest || (st != kByz && r < st)) {
+                v = a.x[j];
+                ++nb;
+            } else if (st == kByz) {
+                ++nz;
+            } else if (r > st) {
+                ++ns;
+            }
+        }
+        sh[j] = v;
+    }
+    // wavefront sums first: 1024 LDS atomics on one address serialise
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        nb += __shfl_xor(nb, o, 64);
+        nz += __shfl_xor(nz, o, 64);
+        ns += __shfl_xor(ns, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&cnt[0], nb);
+        atomicAdd(&cnt[1], nz);
+        atomicAdd(&cnt[2], ns);
+    }
+    __syncthreads();
+    constexpr int EMAX = kGenericMaxM / kDenseSortBlock;   // 8
+    const uint32_t E = (P + kDenseSortBlock - 1) / kDenseSortBlock;
+    const uint32_t tid = threadIdx.x;
+    double v[EMAX];
+    dense_bitonic<EMAX>(sh, P, v);
 #pragma unroll
     for (int e = 0; e < EMAX; ++e) {
         const uint32_t idx = tid + kDenseSortBlock * e;
@@ -153,6 +161,70 @@ struct Merged {   // M = B with two constant blocks (v1 <= v2) spliced in at the
     }
 };
 
+// A sorted sequence made of three constant runs: v[0] on [0, e[0]), v[1] on [e[0], e[1]), v[2] on
+// [e[1], m).  After one persistent round every active node holds its class value, so a
+// receiver's sequence is the class values of the base plus its Byzantine block: three runs.
+struct Runs3 {
+    double v[3];
+    uint32_t e[2];
+    __device__ __forceinline__ double at(uint32_t k) const { return k < e[0] ? v[0] : k < e[1] ? v[1] : v[2]; }
+};
+
+// The rule over the window R = M[t, m - t) of one receiver's merged sorted sequence, by one
+// wavefront (§A.7 stride-halving tree sum spread over the 64 lanes); every lane returns the result.
+template <typename Seq>
+__device__ __forceinline__ double dense_window(const Seq& M, uint32_t rule, uint32_t m, uint32_t t, uint32_t lane) {
+    const uint32_t nr = m - 2 * t;
+    double res;
+    if (rule == 2) {
+        res = (M.at(t) + M.at(m - t - 1)) * 0.5;
+    } else {
+        const uint32_t step = rule == 3 ? t : 1;
+        const uint32_t cnt = rule == 3 ? (nr + t - 1) / t : nr;
+        uint32_t P2 = 64;
+        while (P2 < cnt) P2 <<= 1;
+        // §A.7 stride halving over P2 slots: this lane owns w[lane + 64a]
+        const uint32_t per = P2 / 64;   // <= 128 for m <= 8192
+        double w[8];
+        // levels with stride >= 64 fold in registers: accumulate slot groups in tree order
+        // (per <= 8 keeps the whole lane column in registers; larger P2 folds first)
+        uint32_t per_eff = per;
+        double acc_big = 0.0;
+        (void)acc_big;
+        if (per <= 8) {
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                const uint32_t k = lane + 64u * g;
+                w[g] = (g < (int)per && k < cnt) ? M.at(t + k * step) : 0.0;
+            }
+            for (uint32_t s = per >> 1; s >= 1; s >>= 1) {
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    if ((uint32_t)g < s) w[g] = w[g] + w[g + s];
+            }
+        } else {
+            // large windows: strided partial trees per lane, folded in the same order
+            // (position k = lane + 64*g pairs with k + P2/2 = lane + 64*(g + per/2))
+            double col[128];
+            for (uint32_t g = 0; g < per_eff; ++g) {
+                const uint32_t k = lane + 64u * g;
+                col[g] = k < cnt ? M.at(t + k * step) : 0.0;
+            }
+            for (uint32_t s = per_eff >> 1; s >= 1; s >>= 1)
+                for (uint32_t g = 0; g < s; ++g) col[g] = col[g] + col[g + s];
+            w[0] = col[0];
+        }
+        double v = w[0];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const double u = __shfl_down(v, o, 64);
+            if (lane < (uint32_t)o) v = v + u;
+        }
+        res = readlane_f64(v, 0) / (double)cnt;
+    }
+    return res;
+}
+
 __global__ __launch_bounds__(kDenseRecvBlock) void k_dense_recv(const DenseArgs a) {
     extern __shared__ __attribute__((aligned(16))) double shB[];   // the sorted base multiset
     InstState* S = a.st;
@@ -184,53 +256,7 @@ __global__ __launch_bounds__(kDenseRecvBlock) void k_dense_recv(const DenseArgs 
             M.r1 = M.n1 ? rank_below(shB, nb, M.v1) : 0;
             M.r2 = M.n2 ? rank_below(shB, nb, M.v2) : M.r1;
             if (M.r2 < M.r1) M.r2 = M.r1;
-            const uint32_t m = a.N, t = a.trim, nr = m - 2 * t;
-            if (a.rule == 2) {
-                res = (M.at(t) + M.at(m - t - 1)) * 0.5;
-            } else {
-                const uint32_t step = a.rule == 3 ? t : 1;
-                const uint32_t cnt = a.rule == 3 ? (nr + t - 1) / t : nr;
-                uint32_t P2 = 64;
-                while (P2 < cnt) P2 <<= 1;
-                // §A.7 stride halving over P2 slots: this lane owns w[lane + 64a]
-                const uint32_t per = P2 / 64;   // <= 128 for m <= 8192
-                double w[8];
-                // levels with stride >= 64 fold in registers: accumulate slot groups in tree order
-                // (per <= 8 keeps the whole lane column in registers; larger P2 folds first)
-                uint32_t per_eff = per;
-                double acc_big = 0.0;
-                (void)acc_big;
-                if (per <= 8) {
-#pragma unroll
-                    for (int g = 0; g < 8; ++g) {
-                        const uint32_t k = lane + 64u * g;
-                        w[g] = (g < (int)per && k < cnt) ? M.at(t + k * step) : 0.0;
-                    }
-                    for (uint32_t s = per >> 1; s >= 1; s >>= 1) {
-#pragma unroll
-                        for (int g = 0; g < 4; ++g)
-                            if ((uint32_t)g < s) w[g] = w[g] + w[g + s];
-                    }
-                } else {
-                    // large windows: strided partial trees per lane, folded in the same order
-                    // (position k = lane + 64*g pairs with k + P2/2 = lane + 64*(g + per/2))
-                    double col[128];
-                    for (uint32_t g = 0; g < per_eff; ++g) {
-                        const uint32_t k = lane + 64u * g;
-                        col[g] = k < cnt ? M.at(t + k * step) : 0.0;
-                    }
-                    for (uint32_t s = per_eff >> 1; s >= 1; s >>= 1)
-                        for (uint32_t g = 0; g < s; ++g) col[g] = col[g] + col[g + s];
-                    w[0] = col[0];
-                }
-                double v = w[0];
-#pragma unroll
-                for (int o = 32; o >= 1; o >>= 1) {
-                    const double u = __shfl_down(v, o, 64);
-                    if (lane < (uint32_t)o) v = v + u;
-                }
-                res = readlane_f64(v, 0) / (double)cnt;
-            }
+            res = dense_window(M, a.rule, a.N, a.trim, lane);
             if (st == kHonest) {
                 mn = res;
                 mx = res;
@@ -240,6 +266,164 @@ __global__ __launch_bounds__(kDenseRecvBlock) void k_dense_recv(const DenseArgs 
     }
     // lanes of a receiver agree; fold the block's receivers
     block_minmax_store<kDenseRecvBlock>(mn, mx, a.partial + blockIdx.x);
+}
+
+// Persistent variant: one 1024-thread workgroup per instance runs k rounds in one launch with x
+// resident in LDS (N <= kDensePersistMaxN).  dense_supported() excludes crash faults, so no
+// sender is ever silent and S_i depends on receiver i only through its Byzantine value c_i: the
+// window rule is evaluated once per distinct c (SPLIT: two, by receiver parity; CONSTANT or no
+// faults: one) and broadcast, instead of once per receiver.  Per round: base multiset -> LDS,
+// bitonic sort (dense_bitonic), ≤ 2 window rules, update, honest (min, max), ε test — no
+// launches, no host round trips (cfg2: ≈ 900 rounds).
+__global__ __launch_bounds__(kDenseSortBlock) void k_dense_persist(const BatchArgs a, uint32_t kmax) {
+    __shared__ __attribute__((aligned(16))) double xs[kDensePersistMaxN];
+    __shared__ __attribute__((aligned(16))) double sb[kDensePersistMaxN];
+    __shared__ uint8_t byz[kDensePersistMaxN];   // 1: Byzantine (never updates, never in the base)
+    __shared__ uint32_t cnt[4];                  // base size, #Byzantine, #honest-or-active per parity
+    __shared__ double cls[2];
+    __shared__ double2 red[kDenseSortBlock / 64];
+    const uint32_t lb = blockIdx.x;
+    InstState* S = a.st + lb;
+    if (S->done) return;
+    const uint32_t N = a.N, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint32_t P = 64;
+    while (P < N) P <<= 1;
+    const uint32_t* stv = a.status ? a.status + (uint64_t)lb * N : nullptr;
+    const MsgParams& mp = a.mp;
+    uint32_t r = S->rounds;
+    double lo = S->lo, hi = S->hi, spread = S->spread;
+    bool conv = S->converged != 0, done = false;
+    if (tid < 4) cnt[tid] = 0;
+    __syncthreads();
+    {
+        const double* xin = ((r & 1u) ? a.x1 : a.x0) + (uint64_t)lb * N;
+        uint32_t nz = 0, ne = 0, no = 0;
+        for (uint32_t j = tid; j < N; j += kDenseSortBlock) {
+            xs[j] = xin[j];
+            const bool bz = stv && stv[j] == kByz;
+            byz[j] = bz ? 1 : 0;
+            nz += bz;
+            ne += !bz && !(j & 1u);
+            no += !bz && (j & 1u);
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            nz += __shfl_xor(nz, o, 64);
+            ne += __shfl_xor(ne, o, 64);
+            no += __shfl_xor(no, o, 64);
+        }
+        if (lane == 0) {
+            atomicAdd(&cnt[1], nz);
+            atomicAdd(&cnt[2], ne);
+            atomicAdd(&cnt[3], no);
+        }
+        __syncthreads();
+    }
+    const uint32_t nzv = cnt[1], nbv = N - nzv;
+    const uint32_t ncls = (nzv && mp.byz == 0) ? 2u : 1u;   // SPLIT: parity classes
+    const uint32_t ncnt[2] = {ncls == 2 ? cnt[2] : nbv, ncls == 2 ? cnt[3] : 0u};
+    bool classed = false;   // every non-Byzantine node holds cls[its class] (after one round here)
+    for (uint32_t q = 0; q < kmax && !done; ++q) {
+        if (!classed) {   // base multiset B = values of the non-Byzantine senders, sorted
+            for (uint32_t j = tid; j < P; j += kDenseSortBlock) sb[j] = (j < N && !byz[j]) ? xs[j] : kInf;
+            __syncthreads();
+            constexpr int EP = kDensePersistMaxN / kDenseSortBlock;
+            double v[EP];
+            dense_bitonic<EP>(sb, P, v);
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < EP; ++e) {
+                const uint32_t idx = tid + kDenseSortBlock * e;
+                if (idx < P) sb[idx] = v[e];
+            }
+            __syncthreads();
+        }
+        double res = 0.0;
+        if (w < ncls) {
+            const double c = mp.byz == 0 ? (w == 0 ? hi + mp.delta : lo - mp.delta) : mp.bconst;
+            if (!classed) {
+                Merged M;
+                M.b = sb;
+                M.v1 = c;
+                M.n1 = nzv;
+                M.r1 = nzv ? rank_below(sb, nbv, c) : 0;
+                M.v2 = kInf;
+                M.n2 = 0;
+                M.r2 = M.r1;
+                res = dense_window(M, a.rule, N, a.trim, lane);
+            } else {   // base = {cls0 x n0, cls1 x n1}, plus the Byzantine block {c x nz}
+                double bv[2] = {cls[0], cls[1]};
+                uint32_t bn[2] = {ncnt[0], ncnt[1]};
+                if (ncls == 2 && bv[1] < bv[0]) {
+                    const double tv = bv[0]; bv[0] = bv[1]; bv[1] = tv;
+                    const uint32_t tn = bn[0]; bn[0] = bn[1]; bn[1] = tn;
+                }
+                // insert the Byzantine block before the first base run with a value >= c
+                Runs3 R;
+                if (nzv == 0 || c <= bv[0]) {
+                    R.v[0] = c; R.v[1] = bv[0]; R.v[2] = bv[1];
+                    R.e[0] = nzv; R.e[1] = nzv + bn[0];
+                } else if (ncls == 1 || c <= bv[1]) {
+                    R.v[0] = bv[0]; R.v[1] = c; R.v[2] = bv[1];
+                    R.e[0] = bn[0]; R.e[1] = bn[0] + nzv;
+                } else {
+                    R.v[0] = bv[0]; R.v[1] = bv[1]; R.v[2] = c;
+                    R.e[0] = bn[0]; R.e[1] = bn[0] + bn[1];
+                }
+                res = dense_window(R, a.rule, N, a.trim, lane);
+            }
+        }
+        __syncthreads();   // every class read cls before it is overwritten
+        if (w < ncls && lane == 0) cls[w] = res;
+        __syncthreads();
+        double mn = kInf, mx = -kInf;
+        for (uint32_t i = tid; i < N; i += kDenseSortBlock) {
+            if (byz[i]) continue;   // Byzantine nodes never update
+            const double nv = cls[ncls == 2 ? (i & 1u) : 0u];
+            xs[i] = nv;
+            if (!stv || stv[i] == kHonest) {
+                mn = __builtin_fmin(mn, nv);
+                mx = __builtin_fmax(mx, nv);
+            }
+        }
+        classed = true;
+        mn = wave_min(mn);
+        mx = wave_max(mx);
+        if (lane == 0) red[w] = make_double2(mn, mx);
+        __syncthreads();
+        mn = red[0].x;
+        mx = red[0].y;
+#pragma unroll
+        for (int k = 1; k < kDenseSortBlock / 64; ++k) {
+            mn = __builtin_fmin(mn, red[k].x);
+            mx = __builtin_fmax(mx, red[k].y);
+        }
+        r += 1;
+        lo = mn;
+        hi = mx;
+        spread = hi - lo;
+        if (a.trace && tid == 0) a.trace[(uint64_t)lb * a.trace_stride + r] = spread;
+        conv = spread <= a.eps;
+        done = (a.term_eps && conv) || r >= a.max_rounds;
+        __syncthreads();   // red is rewritten next round
+    }
+    double* xout = ((r & 1u) ? a.x1 : a.x0) + (uint64_t)lb * N;
+    for (uint32_t j = tid; j < N; j += kDenseSortBlock) xout[j] = xs[j];
+    if (tid == 0) {
+        S->lo = lo;
+        S->hi = hi;
+        S->spread = spread;
+        S->rounds = r;
+        S->converged = conv ? 1u : 0u;
+        S->done = done ? 1u : 0u;
+        if (done) atomicAdd(a.n_done, 1u);
+    }
+}
+
+hipError_t launch_dense_persist(const BatchArgs& a, uint64_t B, uint32_t k, hipStream_t s) {
+    if (a.N > kDensePersistMaxN) return hipErrorNotSupported;
+    hipLaunchKernelGGL(k_dense_persist, dim3((unsigned)B), dim3(kDenseSortBlock), 0, s, a, k);
+    return hipGetLastError();
 }
 
 bool dense_supported(uint32_t fault_model, uint32_t byz, uint32_t rule, uint32_t thr, uint64_t N) {

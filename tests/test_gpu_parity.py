@@ -215,3 +215,25 @@ def test_kernel_timing_counts_round_launches():
         s.run()
         ms, n, name = s.kernel_timing()
         assert n == 12 and ms > 0 and (name.startswith("k_round_regular<32,5") or name.startswith("k_bin_scatter+k_bin_gather<32,5>"))
+
+
+@pytest.mark.parametrize("name", ["cfg2_full", "dense300_clean_trim", "dense500_const_dlpsw"])
+def test_dense_two_kernel_path_still_exact(oracle_mod, name, monkeypatch):
+    """The per-round dense kernels (k_dense_sort + k_dense_recv, used above 4096 nodes) on the
+    configs the persistent kernel now serves."""
+    monkeypatch.setenv("ACSIM_DENSE_PERSIST", "0")
+    cfg = CASES[name]
+    with acsim.Simulator(cfg, device=0) as g:
+        assert g.kernel_name() == "k_dense_sort+k_dense_recv"
+    g, o = run_both(oracle_mod, cfg)
+    assert_same(g, o)
+
+
+def test_dense_persistent_multi_instance(oracle_mod):
+    cfg = Config(n_nodes=700, n_instances=5, topology="complete", rule="trimmed", trim=200,
+                 fault_model="byzantine", n_faulty=200, byz_strategy="split", byz_delta=0.01,
+                 eps=1e-9, max_rounds=2000, seed=41, instance_offset=3, trace_spread=True)
+    with acsim.Simulator(cfg, device=0) as g:
+        assert g.kernel_name() == "k_dense_persist"
+    g, o = run_both(oracle_mod, cfg)
+    assert_same(g, o)
