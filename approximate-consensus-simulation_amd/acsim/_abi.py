@@ -20,7 +20,7 @@ BACKEND_CPU, BACKEND_HIP = 0, 1
 
 # topology / rule / faults / byz / termination / dtype
 TOPO_COMPLETE, TOPO_RANDOM_REGULAR, TOPO_CSR = 0, 1, 2
-RULE_AVERAGE, RULE_TRIMMED_MEAN, RULE_MIDPOINT, RULE_DLPSW_SELECT = 0, 1, 2, 3
+RULE_AVERAGE, RULE_TRIMMED_MEAN, RULE_MIDPOINT, RULE_DLPSW_SELECT, RULE_WMSR = 0, 1, 2, 3, 4
 FAULT_NONE, FAULT_CRASH, FAULT_BYZANTINE = 0, 1, 2
 BYZ_SPLIT, BYZ_RANDOM, BYZ_CONSTANT = 0, 1, 2
 TERM_EPS, TERM_FIXED = 0, 1

@@ -16,7 +16,8 @@ _ENUMS = {
                  "regular": _abi.TOPO_RANDOM_REGULAR, "csr": _abi.TOPO_CSR},
     "rule": {"average": _abi.RULE_AVERAGE, "trimmed_mean": _abi.RULE_TRIMMED_MEAN,
              "trimmed": _abi.RULE_TRIMMED_MEAN, "midpoint": _abi.RULE_MIDPOINT,
-             "dlpsw": _abi.RULE_DLPSW_SELECT, "dlpsw_select": _abi.RULE_DLPSW_SELECT},
+             "dlpsw": _abi.RULE_DLPSW_SELECT, "dlpsw_select": _abi.RULE_DLPSW_SELECT,
+             "wmsr": _abi.RULE_WMSR, "w_msr": _abi.RULE_WMSR},
     "fault_model": {"none": _abi.FAULT_NONE, "crash": _abi.FAULT_CRASH,
                     "byzantine": _abi.FAULT_BYZANTINE},
     "byz_strategy": {"split": _abi.BYZ_SPLIT, "random": _abi.BYZ_RANDOM,

@@ -127,7 +127,7 @@ static int validate(const acs_config* c) {
     }
     if (slots >= (1ull << 34)) return fail(ACS_EINVAL, "slot count must be < 2^34");
     if (c->topology == ACS_TOPO_CSR) {
-        if (c->rule > ACS_RULE_DLPSW_SELECT) return fail(ACS_EINVAL, "unknown rule %u", c->rule);
+        if (c->rule > ACS_RULE_WMSR) return fail(ACS_EINVAL, "unknown rule %u", c->rule);
         if (c->rule == ACS_RULE_AVERAGE && c->trim != 0) return fail(ACS_EINVAL, "AVERAGE requires trim == 0");
         if (c->rule == ACS_RULE_DLPSW_SELECT && c->trim < 1) return fail(ACS_EINVAL, "DLPSW needs t >= 1");
     } else
@@ -137,6 +137,7 @@ static int validate(const acs_config* c) {
             break;
         case ACS_RULE_TRIMMED_MEAN:
         case ACS_RULE_MIDPOINT:
+        case ACS_RULE_WMSR:
             if (m <= 2ull * c->trim) return fail(ACS_EINVAL, "need m > 2t");
             break;
         case ACS_RULE_DLPSW_SELECT:

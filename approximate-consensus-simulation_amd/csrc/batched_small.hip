@@ -158,12 +158,24 @@ __global__ __launch_bounds__(64) void k_batched_small(const BatchArgs a, uint32_
             if (a.rule == 2) {
                 res = (colbuf[t * 64 + lane] + colbuf[(N - t - 1) * 64 + lane]) * 0.5;
             } else {
-                const uint32_t step = a.rule == 3 ? t : 1;
-                const uint32_t cnt = a.rule == 3 ? (nr + t - 1) / t : nr;
+                uint32_t start = t, step = a.rule == 3 ? t : 1;
+                uint32_t cnt = a.rule == 3 ? (nr + t - 1) / t : nr;
+                if (a.rule == 4) {   // W-MSR: window [min(t, #below), N - min(t, #above))
+                    uint32_t nl = 0, ng = 0;
+                    for (uint32_t k = 0; k < N; ++k) {
+                        const double u = colbuf[k * 64 + lane];
+                        nl += u < xi;
+                        ng += u > xi;
+                    }
+                    const uint32_t wlo = nl < t ? nl : t, whi = ng < t ? ng : t;
+                    start = wlo;
+                    step = 1;
+                    cnt = N - wlo - whi;
+                }
                 uint32_t P2 = 1;
                 while (P2 < cnt) P2 <<= 1;
-                for (uint32_t k = 0; k < P2; ++k)   // in place: source index t + k*step >= k
-                    colbuf[k * 64 + lane] = k < cnt ? colbuf[(t + k * step) * 64 + lane] : 0.0;
+                for (uint32_t k = 0; k < P2; ++k)   // in place: source index start + k*step >= k
+                    colbuf[k * 64 + lane] = k < cnt ? colbuf[(start + k * step) * 64 + lane] : 0.0;
                 for (uint32_t s2 = P2 >> 1; s2 >= 1; s2 >>= 1)
                     for (uint32_t k = 0; k < s2; ++k)
                         colbuf[k * 64 + lane] = colbuf[k * 64 + lane] + colbuf[(k + s2) * 64 + lane];

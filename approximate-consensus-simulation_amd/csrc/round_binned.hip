@@ -134,7 +134,7 @@ __global__ __launch_bounds__(kBinA) void k_bin_regroup(const double* __restrict_
 // ------------------------------------------------------------------------------ phase B
 // The runs of block b (run j of a table row of nrun + 1 descriptors) are copied into LDS,
 // concatenated; lane i_local then reads its D values at invpos[b][t][i_local].
-template <int D, int T>
+template <int D, int T, bool WMSR = false>
 __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const double* __restrict__ stage,
                                                        const uint16_t* __restrict__ invpos,
                                                        const uint2* __restrict__ tiles, uint32_t nrun, uint32_t Q,
@@ -178,7 +178,7 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
                 v[2 + 8 * q + 2 * e] = raw[wd[e] >> 16];
             }
         }
-        const double res = apply_rule_reg<D, T>(a.rule, v);
+        const double res = apply_rule_reg<D, T, WMSR>(a.rule, v);
         a.xout[i] = res;
         mn = res;
         mx = res;
@@ -346,7 +346,7 @@ __global__ __launch_bounds__(256) void k_bin_inv(uint64_t E, BinGeom G, uint32_t
 #define ACS_BINNED_VARIANTS(X) X(16, 5) X(32, 5) X(16, 0) X(32, 0) X(8, 2) X(8, 0)
 
 bool binned_supported(uint32_t d, uint32_t t, uint32_t rule) {
-    if (rule != 1 && rule != 2 && rule != 3) return false;   // sort-based rules only
+    if (rule < 1 || rule > 4) return false;   // sort-based rules only (W-MSR also reads x_i, which phase B has)
     if (rule == 3 && t < 1) return false;
 #define X(DD, TT) if (d == DD && t == TT) return true;
     ACS_BINNED_VARIANTS(X)
@@ -602,8 +602,12 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, hipStrea
     const dim3 grid(8 * Qc);
 #define X(DD, TT)                                                                                        \
     if (p.D == DD && a.trim == TT) {                                                                     \
-        hipLaunchKernelGGL((k_bin_gather<DD, TT>), grid, dim3(kBinSB), 0, s, a, last, p.invpos, p.tiles, \
-                           p.nrun, p.Q, Qc);                                                             \
+        if (a.rule == 4)                                                                                 \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, true>), grid, dim3(kBinSB), 0, s, a, last, p.invpos,   \
+                               p.tiles, p.nrun, p.Q, Qc);                                                \
+        else                                                                                             \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT>), grid, dim3(kBinSB), 0, s, a, last, p.invpos, p.tiles, \
+                               p.nrun, p.Q, Qc);                                                         \
         return hipGetLastError();                                                                        \
     }
     ACS_BINNED_VARIANTS(X)

@@ -427,7 +427,7 @@ hipError_t launch_dense_persist(const BatchArgs& a, uint64_t B, uint32_t k, hipS
 }
 
 bool dense_supported(uint32_t fault_model, uint32_t byz, uint32_t rule, uint32_t thr, uint64_t N) {
-    if (thr != 0 || rule == 0 || N > kGenericMaxM || N < 2) return false;
+    if (thr != 0 || rule == 0 || rule == 4 || N > kGenericMaxM || N < 2) return false;   // W-MSR: per-x_i windows
     if (fault_model == 1) return false;   // crash rounds deliver per slot: generic kernel
     if (fault_model == 2 && byz == 1) return false;   // RANDOM Byzantine values are per slot
     return true;

@@ -109,7 +109,25 @@ __global__ __launch_bounds__(kGenericBlock) void k_round_generic(const RoundArgs
     } else {
         block_bitonic_sort(sh, P);
         const uint32_t t = a.trim, nr = m - 2 * t;
-        if (a.rule == 2) {
+        if (a.rule == 4) {   // W-MSR: window [min(t, #below), m - min(t, #above))
+            uint32_t nl = 0, nle = 0;   // #entries < xi, #entries <= xi (sh is sorted)
+            {
+                uint32_t lo_ = 0, hi_ = m;
+                while (lo_ < hi_) { const uint32_t md = (lo_ + hi_) >> 1; if (sh[md] < xi) lo_ = md + 1; else hi_ = md; }
+                nl = lo_;
+                hi_ = m;
+                while (lo_ < hi_) { const uint32_t md = (lo_ + hi_) >> 1; if (sh[md] <= xi) lo_ = md + 1; else hi_ = md; }
+                nle = lo_;
+            }
+            const uint32_t ng = m - nle;
+            const uint32_t wlo = nl < t ? nl : t, whi = ng < t ? ng : t, cnt = m - wlo - whi;
+            uint32_t P2 = 1;
+            while (P2 < cnt) P2 <<= 1;
+            double* w = sh + P;
+            for (uint32_t k = threadIdx.x; k < P2; k += kGenericBlock) w[k] = k < cnt ? sh[wlo + k] : 0.0;
+            __syncthreads();
+            res = block_tree_sum(w, P2) / (double)cnt;
+        } else if (a.rule == 2) {
             res = (sh[t] + sh[m - t - 1]) * 0.5;
         } else {
             const uint32_t step = a.rule == 3 ? t : 1;

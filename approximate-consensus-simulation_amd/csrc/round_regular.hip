@@ -17,7 +17,7 @@
 
 namespace acs {
 
-template <int D, int T, bool CLEAN>
+template <int D, int T, bool CLEAN, bool WMSR = false>
 __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs a) {
     static_assert(D % 4 == 0, "compiled degrees are multiples of 4");
     constexpr int M = D + 1;
@@ -100,7 +100,7 @@ __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs
                     }
                 }
             }
-            res = apply_rule_reg<D, T>(a.rule, v);
+            res = apply_rule_reg<D, T, WMSR>(a.rule, v);
         }
         xo[i] = res;
         if (honest) {
@@ -119,6 +119,7 @@ __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs
 static bool rule_ok(uint32_t t, uint32_t rule) {
     if (rule == 0) return t == 0;     // AVERAGE
     if (rule == 3) return t >= 1;     // DLPSW
+    if (rule == 4) return true;       // W-MSR
     return rule == 1 || rule == 2;
 }
 
@@ -145,8 +146,13 @@ hipError_t launch_round_regular(const RoundArgs& a, uint64_t B, bool clean, hipS
     const dim3 block(kRegularBlock);
 #define X(DD, TT)                                                                         \
     if (a.d == DD && a.trim == TT) {                                                      \
-        if (clean)                                                                        \
+        const bool w_ = a.rule == 4;                                                      \
+        if (clean && w_)                                                                  \
+            hipLaunchKernelGGL((k_round_regular<DD, TT, true, true>), grid, block, 0, s, a); \
+        else if (clean)                                                                   \
             hipLaunchKernelGGL((k_round_regular<DD, TT, true>), grid, block, 0, s, a);    \
+        else if (w_)                                                                      \
+            hipLaunchKernelGGL((k_round_regular<DD, TT, false, true>), grid, block, 0, s, a); \
         else                                                                              \
             hipLaunchKernelGGL((k_round_regular<DD, TT, false>), grid, block, 0, s, a);   \
         return hipGetLastError();                                                         \

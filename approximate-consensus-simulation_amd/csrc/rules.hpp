@@ -8,9 +8,44 @@ namespace acs {
 
 // v[0..D] holds the m = D+1 resolved entries (entry order for AVERAGE; any order for the
 // sort-based rules, whose result depends only on the multiset).
+// W-MSR over the m = D+1 entries, v[0] = the receiver's own value: full sort,
+// drop min(T, #below) from the bottom and min(T, #above) from the top, tree_sum the window.
+// The window start is a runtime value in [0, T]; zero padding past the window leaves the
+// stride-halving sum unchanged (no -0.0 values), so the compile-time tree over next_pow2(M)
+// equals the spec's tree over next_pow2(window).
 template <int D, int T>
+__device__ __forceinline__ double wmsr_reg(double (&v)[D + 1]) {
+    constexpr int M = D + 1;
+    const double xi = v[0];
+    select_sort<M>(v);
+    uint32_t nl = 0, ng = 0;
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+        nl += v[k] < xi;
+        ng += v[k] > xi;
+    }
+    const uint32_t lo = nl < (uint32_t)T ? nl : (uint32_t)T, hi = ng < (uint32_t)T ? ng : (uint32_t)T;
+    const uint32_t nw = M - lo - hi;
+    double w[M];
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+        double s = v[k];
+#pragma unroll
+        for (int q = 1; q <= T; ++q)
+            if (k + q < M && lo == (uint32_t)q) s = v[k + q];
+        w[k] = (uint32_t)k < nw ? s : 0.0;
+    }
+    return tree_sum_const<M>(w) / (double)nw;
+}
+
+// WMSR = true instantiates the W-MSR rule only (a separate kernel instantiation, so the other
+// rules' kernels carry none of its registers).
+template <int D, int T, bool WMSR = false>
 __device__ __forceinline__ double apply_rule_reg(uint32_t rule, double (&v)[D + 1]) {
     constexpr int M = D + 1;
+    if constexpr (WMSR) {
+        return wmsr_reg<D, T>(v);
+    }
     if constexpr (T == 0) {
         if (rule == 0) return tree_sum_const<M>(v) / (double)M;   // AVERAGE: entry order
     }

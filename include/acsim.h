@@ -51,6 +51,9 @@ extern "C" {
 #define ACS_RULE_TRIMMED_MEAN  1
 #define ACS_RULE_MIDPOINT      2
 #define ACS_RULE_DLPSW_SELECT  3
+/* W-MSR (LeBlanc et al. 2013): drop up to t entries strictly below the receiver's
+ * own value (the smallest ones) and up to t strictly above it (the largest), average the rest */
+#define ACS_RULE_WMSR          4
 
 /* fault model (§A.4) */
 #define ACS_FAULT_NONE       0

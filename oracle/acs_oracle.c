@@ -154,10 +154,22 @@ static void sort_asc(double* a, uint64_t m) {
     }
 }
 
-/* §A.7: apply the rule to the m entries of S (S is reordered in place). */
-static double apply_rule(uint32_t rule, uint32_t t, double* S, uint64_t m, double* scratch) {
+/* §A.7: apply the rule to the m entries of S (S is reordered in place); xi is the receiver's own
+ * value (W-MSR only). */
+static double apply_rule(uint32_t rule, uint32_t t, double* S, uint64_t m, double* scratch, double xi) {
     if (rule == ACS_RULE_AVERAGE) return acso_tree_sum(S, m) / (double)m;
     sort_asc(S, m);
+    if (rule == ACS_RULE_WMSR) {
+        /* drop min(t, #below) smallest and min(t, #above) largest entries, where
+         * below / above are strictly less / greater than xi; tree_sum the rest in sorted order */
+        uint64_t nl = 0, ng = 0;
+        for (uint64_t k = 0; k < m; ++k) {
+            if (S[k] < xi) ++nl;
+            else if (S[k] > xi) ++ng;
+        }
+        const uint64_t lo = nl < t ? nl : t, hi = ng < t ? ng : t, nw = m - lo - hi;
+        return acso_tree_sum(S + lo, nw) / (double)nw;
+    }
     const double* R = S + t;
     const uint64_t nr = m - 2ull * t;
     if (rule == ACS_RULE_TRIMMED_MEAN) return acso_tree_sum(R, nr) / (double)nr;
@@ -195,7 +207,7 @@ int acso_validate(const acs_config* c) {
     }
     if (slots >= (1ull << 34)) return fail(ACS_EINVAL, "slot count must be < 2^34");
     if (c->topology == ACS_TOPO_CSR) {
-        if (c->rule > ACS_RULE_DLPSW_SELECT) return fail(ACS_EINVAL, "unknown rule %u", c->rule);
+        if (c->rule > ACS_RULE_WMSR) return fail(ACS_EINVAL, "unknown rule %u", c->rule);
         if (c->rule == ACS_RULE_AVERAGE && c->trim != 0) return fail(ACS_EINVAL, "AVERAGE requires trim == 0");
         if (c->rule == ACS_RULE_DLPSW_SELECT && c->trim < 1) return fail(ACS_EINVAL, "DLPSW needs t >= 1");
     } else
@@ -205,6 +217,7 @@ int acso_validate(const acs_config* c) {
             break;
         case ACS_RULE_TRIMMED_MEAN:
         case ACS_RULE_MIDPOINT:
+        case ACS_RULE_WMSR:
             if (m <= 2ull * c->trim) return fail(ACS_EINVAL, "need m > 2t");
             break;
         case ACS_RULE_DLPSW_SELECT:
@@ -480,7 +493,7 @@ static void step_instance(acso_sim* s, uint64_t lb) {
                 S[0] = x[i];
                 for (uint64_t t = 0; t < deg; ++t)
                     S[1 + t] = resolve(s, b, bG, r, x, st, i, s->colidx[rp + t], rp + t, lo, hi);
-                xn[i] = apply_rule(c->rule, c->trim, S, deg + 1, scratch);
+                xn[i] = apply_rule(c->rule, c->trim, S, deg + 1, scratch, x[i]);
                 continue;
             } else {
                 const uint64_t d = c->degree;
@@ -488,7 +501,7 @@ static void step_instance(acso_sim* s, uint64_t lb) {
                 for (uint64_t t = 0; t < d; ++t)
                     S[1 + t] = resolve(s, b, bG, r, x, st, i, s->nbr[i * d + t], i * d + t, lo, hi);
             }
-            xn[i] = apply_rule(c->rule, c->trim, S, m, scratch);
+            xn[i] = apply_rule(c->rule, c->trim, S, m, scratch, x[i]);
         }
         free(S);
     }

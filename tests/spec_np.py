@@ -109,11 +109,23 @@ def tree_sum_rows(a: np.ndarray) -> np.ndarray:
     return w[..., 0]
 
 
-def apply_rule(rule: int, t: int, S: np.ndarray) -> np.ndarray:
-    """§A.7 on rows of S (entry order preserved for AVERAGE)."""
+def apply_rule(rule: int, t: int, S: np.ndarray, xi=None) -> np.ndarray:
+    """§A.7 on rows of S (entry order preserved for AVERAGE); xi = receivers' own values (W-MSR)."""
     m = S.shape[1]
     if rule == 0:
         return tree_sum_rows(S) / float(m)
+    if rule == 4:
+        # W-MSR (DESIGN.md §9): drop min(t, #below x_i) smallest and min(t, #above x_i) largest;
+        # zero padding past the window leaves the stride-halving sum unchanged (no -0.0 values)
+        Ss = np.sort(S, axis=1)
+        xi = np.asarray(xi, dtype=np.float64)[:, None]
+        lo = np.minimum(t, (Ss < xi).sum(axis=1))
+        hi = np.minimum(t, (Ss > xi).sum(axis=1))
+        nw = m - lo - hi
+        k = np.arange(m)[None, :]
+        idx = np.minimum(lo[:, None] + k, m - 1)
+        W = np.where(k < nw[:, None], np.take_along_axis(Ss, idx, axis=1), 0.0)
+        return tree_sum_rows(W) / nw.astype(np.float64)
     R = np.sort(S, axis=1)[:, t:m - t]
     if rule == 1:
         return tree_sum_rows(R) / float(R.shape[1])
@@ -208,7 +220,7 @@ class NpSim:
                 selfm = np.zeros(J.shape, dtype=bool)
                 selfm[0, 0] = True
                 V = self._values(np.array([i]), J, slots, selfm, r, b, bG, x, st, lo, hi)
-                xn[i] = apply_rule(self.rule, self.t, V)[0]
+                xn[i] = apply_rule(self.rule, self.t, V, x[[i]])[0]
         elif A.size:
             if self.topo == 0:
                 J = np.broadcast_to(np.arange(N), (A.size, N))
@@ -223,7 +235,7 @@ class NpSim:
                 selfm = np.zeros(J.shape, dtype=bool)
                 selfm[:, 0] = True
             V = self._values(A, J, slots, selfm, r, b, bG, x, st, lo, hi)
-            xn[A] = apply_rule(self.rule, self.t, V)
+            xn[A] = apply_rule(self.rule, self.t, V, x[A])
         self.x[lb] = xn
         self.rounds[lb] = r + 1
         self._after(lb)

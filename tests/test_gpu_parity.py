@@ -88,6 +88,22 @@ CASES = {
     "reg4_t1_multi_instance": Config(n_nodes=5000, n_instances=5, topology="regular", degree=4,
                                      rule="trimmed", trim=1, loss_p=0.1, mask_group=2, eps=1e-6,
                                      max_rounds=3000, seed=12, instance_offset=9, trace_spread=True),
+    # W-MSR through every kernel family
+    "wmsr_reg16_t5_byzrandom_drop": Config(n_nodes=30000, topology="regular", degree=16, rule="wmsr",
+                                           trim=5, fault_model="byzantine", n_faulty=900,
+                                           byz_strategy="random", byz_delta=0.2, loss_p=0.1,
+                                           eps=1e-8, max_rounds=300, seed=51, trace_spread=True),
+    "wmsr_reg32_t5_clean_binned": Config(n_nodes=60000, topology="regular", degree=32, rule="wmsr", trim=5,
+                                         eps=1e-10, max_rounds=300, seed=52, trace_spread=True),
+    "wmsr_generic_reg12_t3_crash": Config(n_nodes=5000, topology="regular", degree=12, rule="wmsr", trim=3,
+                                          fault_model="crash", n_faulty=80, crash_window=5, eps=1e-8,
+                                          max_rounds=400, seed=53, trace_spread=True),
+    "wmsr_complete200_split": Config(n_nodes=200, topology="complete", rule="wmsr", trim=30,
+                                     fault_model="byzantine", n_faulty=30, byz_strategy="split",
+                                     byz_delta=0.1, eps=1e-9, max_rounds=500, seed=54, trace_spread=True),
+    "wmsr_batched40_crash_drop": Config(n_nodes=40, n_instances=20, topology="complete", rule="wmsr",
+                                        trim=6, fault_model="crash", n_faulty=5, crash_window=4,
+                                        loss_p=0.2, eps=1e-10, max_rounds=300, seed=55, trace_spread=True),
     # generic kernel (odd d / t, dense complete graphs)
     "generic_reg10_t3": Config(n_nodes=7000, topology="regular", degree=10, rule="trimmed", trim=3,
                                fault_model="crash", n_faulty=100, crash_window=6, loss_p=0.05,

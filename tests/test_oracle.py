@@ -115,7 +115,13 @@ def test_oracle_reproduces_golden(oracle_mod, name):
            trace_spread=True),
     Config(n_nodes=10, n_instances=7, topology="complete", rule="average", loss_p=0.4, mask_group=3,
            eps=0.0, max_rounds=25, termination="fixed", seed=2, trace_spread=True),
-], ids=["complete_mid_crash_drop", "regular_dlpsw_split", "batched_avg_fixed_grouped"])
+    Config(n_nodes=400, topology="regular", degree=16, rule="wmsr", trim=4, fault_model="byzantine",
+           n_faulty=30, byz_strategy="random", byz_delta=0.3, loss_p=0.1, eps=1e-9, max_rounds=300,
+           seed=13, trace_spread=True),
+    Config(n_nodes=40, topology="complete", rule="wmsr", trim=6, fault_model="crash", n_faulty=5,
+           crash_window=4, eps=1e-10, max_rounds=300, seed=14, trace_spread=True),
+], ids=["complete_mid_crash_drop", "regular_dlpsw_split", "batched_avg_fixed_grouped",
+        "regular_wmsr_byzrandom_drop", "complete_wmsr_crash"])
 def test_oracle_matches_numpy(oracle_mod, cfg):
     with oracle_mod.OracleSimulator(cfg) as o:
         o.run()
