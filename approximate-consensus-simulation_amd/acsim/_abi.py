@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # status codes
 OK, EINVAL, ENOMEM, EDEVICE, ECOMM, EUNSUPPORTED = 0, -1, -2, -3, -4, -5
@@ -59,6 +59,8 @@ class AcsConfig(C.Structure):
         ("trace_spread", C.c_uint32),
         ("omp_threads", C.c_uint32),
         ("instance_offset", C.c_uint64),
+        ("delay_max", C.c_uint32),
+        ("reserved0", C.c_uint32),
     ]
 
 

@@ -63,6 +63,7 @@ class Config:
     trace_spread: bool = False
     omp_threads: int = 0
     instance_offset: int = 0
+    delay_max: int = 0          # bounded-delay rounds; 0 = synchronous
 
     def replace(self, **kw) -> "Config":
         return dataclasses.replace(self, **kw)
@@ -98,6 +99,7 @@ class Config:
         c.trace_spread = 1 if self.trace_spread else 0
         c.omp_threads = int(self.omp_threads)
         c.instance_offset = int(self.instance_offset)
+        c.delay_max = int(self.delay_max)
         return c
 
 

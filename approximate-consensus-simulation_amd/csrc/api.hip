@@ -68,7 +68,10 @@ struct acs_sim {
     bool dense_persist = false;    // PATH_DENSE served by the persistent LDS-resident kernel
     BinnedPlan bin{};
     MsgParams mp{};
-    double* x[2] = {nullptr, nullptr};
+    double* x[2] = {nullptr, nullptr};   // x[k] = xb(k): the synchronous double buffer
+    double* xall = nullptr;        // H value buffers of B*Npad (+2) doubles, x^q in buffer q % H
+    uint64_t xstride = 0;          // elements per buffer
+    uint32_t H = 2;                // delay_max + 2: x^{r-D} .. x^r read, x^{r+1} written
     uint32_t* ell = nullptr;       // rows [row0, row0 + rows_per) of this rank
     uint32_t* status = nullptr;
     InstState* st = nullptr;
@@ -167,6 +170,8 @@ static int validate(const acs_config* c) {
     if (!(c->eps >= 0.0 && c->eps <= 1e300)) return fail(ACS_EINVAL, "eps must be finite, >= 0");
     if (c->termination > ACS_TERM_FIXED) return fail(ACS_EINVAL, "unknown termination");
     if (c->dtype != ACS_F64) return fail(ACS_EUNSUPPORTED, "only ACS_F64 is implemented");
+    if (c->delay_max > 64) return fail(ACS_EINVAL, "delay_max must be <= 64");
+    if (c->reserved0 != 0) return fail(ACS_EINVAL, "reserved0 must be 0");
     if (c->trace_spread && c->n_instances * ((uint64_t)c->max_rounds + 1) > (1ull << 28))
         return fail(ACS_EINVAL, "spread trace too large (B*(max_rounds+1) > 2^28)");
     return ACS_OK;
@@ -198,8 +203,7 @@ static void release(acs_sim* s) {
         (void)hipFree(p.ell);
         binned_free(p.bin);
     }
-    (void)hipFree(s->x[0]);
-    (void)hipFree(s->x[1]);
+    (void)hipFree(s->xall);
     (void)hipFree(s->ell);
     binned_free(s->bin);
     (void)hipFree(s->status);
@@ -216,6 +220,9 @@ static void release(acs_sim* s) {
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
 }
+
+// value buffer holding x^q
+static double* xb(const acs_sim* s, uint32_t q) { return s->xall + (uint64_t)(q % s->H) * s->xstride; }
 
 static FinalizeArgs make_finalize(acs_sim* s, uint32_t r_next, const double2* partial, uint32_t nblk,
                                   bool init) {
@@ -245,7 +252,7 @@ static uint64_t part_rows(const acs_sim* s, int p) {
 // holds the full x, so the initial honest min/max needs no exchange.
 static int init_state(acs_sim* s, uint32_t round) {
     HIP_TRY(hipMemsetAsync(s->n_done, 0, sizeof(uint32_t), s->stream));
-    HIP_TRY(launch_partials_from_x(s->x[round & 1u], s->status, s->B, s->N, s->partial, s->nblk_init, s->stream));
+    HIP_TRY(launch_partials_from_x(xb(s, round), s->status, s->B, s->N, s->partial, s->nblk_init, s->stream));
     const FinalizeArgs f = make_finalize(s, round, s->partial, s->nblk_init, true);
     HIP_TRY(launch_finalize(f, s->B, s->stream));
     HIP_TRY(hipMemcpyAsync(s->h_ndone, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
@@ -293,8 +300,12 @@ static int timing_begin(acs_sim* s, hipEvent_t* e1) {
 
 static RoundArgs round_args(acs_sim* s, uint32_t r) {
     RoundArgs a{};
-    a.xin = s->x[r & 1u];
-    a.xout = s->x[(r + 1) & 1u];
+    a.xin = xb(s, r);
+    a.xout = xb(s, r + 1);
+    a.xh = s->xall;
+    a.xstride = s->xstride;
+    a.H = s->H;
+    a.delay = s->c.delay_max;
     a.ell = s->ell;
     a.status = s->status;
     a.st = s->st;
@@ -541,6 +552,8 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     if (virt && rank != 0) return fail(ACS_EINVAL, "virtual partitions live on one handle (rank 0)");
     if (comm_id && id_len != sizeof(ncclUniqueId))
         return fail(ACS_EINVAL, "comm id must be %zu bytes", sizeof(ncclUniqueId));
+    if (partitioned && cfg->delay_max)
+        return fail(ACS_EUNSUPPORTED, "node partitioning runs synchronous rounds only (delay_max = 0)");
     if (partitioned) {
         if (cfg->topology != ACS_TOPO_RANDOM_REGULAR || cfg->n_instances != 1 ||
             !regular_fast_supported(cfg->degree, cfg->trim, cfg->rule))
@@ -561,7 +574,8 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
                                               : (uint64_t)cfg->degree + 1;
     s->d = cfg->topology == ACS_TOPO_CSR ? 0 : cfg->degree;
     s->dp = (cfg->degree + 3u) & ~3u;
-    s->clean = cfg->fault_model == ACS_FAULT_NONE && drop_threshold(cfg->loss_p) == 0;
+    // "clean": no slot-dependent decision at all (no faults, no loss, no delays)
+    s->clean = cfg->fault_model == ACS_FAULT_NONE && drop_threshold(cfg->loss_p) == 0 && cfg->delay_max == 0;
     s->mp.key = key_of(cfg->seed);
     s->mp.thr = drop_threshold(cfg->loss_p);
     s->mp.fault = cfg->fault_model;
@@ -577,7 +591,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     s->rows_per = partitioned ? ((s->N + nranks - 1) / nranks + 63) / 64 * 64 : s->N;
     s->Npad = partitioned ? s->rows_per * nranks : s->N;
 
-    if (cfg->topology == ACS_TOPO_COMPLETE && s->N <= kBatchedMaxN) {
+    if (cfg->topology == ACS_TOPO_COMPLETE && s->N <= kBatchedMaxN && cfg->delay_max == 0) {
         s->path = PATH_BATCHED;
         s->kname = batched_small_name((uint32_t)s->N, cfg->rule, cfg->fault_model != ACS_FAULT_NONE);
         const char* env = getenv("ACSIM_MFMA");
@@ -585,7 +599,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
                   batched_mfma_supported((uint32_t)s->N, cfg->rule, cfg->fault_model != ACS_FAULT_NONE, cfg->mask_group,
                                          cfg->instance_offset);
         if (s->mfma) s->kname = "k_batched_mfma<v_mfma_f64_16x16x4>";
-    } else if (cfg->topology == ACS_TOPO_COMPLETE && !partitioned &&
+    } else if (cfg->topology == ACS_TOPO_COMPLETE && !partitioned && cfg->delay_max == 0 &&
                (s->B == 1 || (s->N <= kDensePersistMaxN && !env_off("ACSIM_DENSE_PERSIST"))) &&
                dense_supported(cfg->fault_model, cfg->byz_strategy, cfg->rule, s->mp.thr, s->N)) {
         s->path = PATH_DENSE;
@@ -652,8 +666,11 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     CREATE_TRY(hipSetDevice(s->device));
     CREATE_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     const uint64_t xlen = s->B * s->Npad;
-    CREATE_TRY(hipMalloc(&s->x[0], (xlen + 2) * sizeof(double)));   // +2: 16-byte tail reads (binned)
-    CREATE_TRY(hipMalloc(&s->x[1], (xlen + 2) * sizeof(double)));
+    s->H = cfg->delay_max + 2;
+    s->xstride = xlen + 2;   // +2: 16-byte tail reads (binned)
+    CREATE_TRY(hipMalloc(&s->xall, s->H * s->xstride * sizeof(double)));
+    s->x[0] = s->xall;
+    s->x[1] = s->xall + s->xstride;
     CREATE_TRY(hipMalloc(&s->st, s->B * sizeof(InstState)));
     CREATE_TRY(hipMemsetAsync(s->st, 0, s->B * sizeof(InstState), s->stream));
     CREATE_TRY(hipMalloc(&s->partial, s->B * ncap * sizeof(double2)));
@@ -847,7 +864,7 @@ int acs_get_values(acs_sim* s, uint64_t b, void* out, uint64_t n) {
     InstState e;
     HIP_TRY(hipMemcpyAsync(&e, s->st + b, sizeof e, hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
-    HIP_TRY(hipMemcpyAsync(out, s->x[e.rounds & 1u] + b * s->Npad, s->N * sizeof(double), hipMemcpyDeviceToHost,
+    HIP_TRY(hipMemcpyAsync(out, xb(s, e.rounds) + b * s->Npad, s->N * sizeof(double), hipMemcpyDeviceToHost,
                            s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     return ACS_OK;
@@ -914,8 +931,10 @@ int acs_set_state(acs_sim* s, uint32_t round, const void* x, uint64_t n) {
     HIP_TRY(hipSetDevice(s->device));
     const double* hx = (const double*)x;
     for (uint64_t b = 0; b < s->B; ++b) {
-        HIP_TRY(hipMemcpyAsync(s->x[round & 1u] + b * s->Npad, hx + b * s->N, s->N * sizeof(double),
-                               hipMemcpyHostToDevice, s->stream));
+        // every delay-history buffer restarts from x; one buffer when synchronous
+        for (uint32_t q = 0; q < (s->c.delay_max ? s->H : 1u); ++q)
+            HIP_TRY(hipMemcpyAsync((s->c.delay_max ? s->xall + q * s->xstride : xb(s, round)) + b * s->Npad,
+                                   hx + b * s->N, s->N * sizeof(double), hipMemcpyHostToDevice, s->stream));
         for (Part& q : s->parts)
             HIP_TRY(hipMemcpyAsync(q.x[round & 1u] + b * s->Npad, hx + b * s->N, s->N * sizeof(double),
                                    hipMemcpyHostToDevice, s->stream));

@@ -45,6 +45,10 @@ struct RoundArgs {
     uint32_t r;               // round being produced: x^r -> x^{r+1}
     uint32_t nblk;            // partial blocks per instance
     MsgParams mp;
+    // bounded-delay rounds: x^q lives at xh + (q % H) * xstride (instance-major)
+    const double* xh;
+    uint64_t xstride;
+    uint32_t H, delay;        // delay = D (0: synchronous)
 };
 
 struct FinalizeArgs {

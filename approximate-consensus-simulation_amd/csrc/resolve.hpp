@@ -18,6 +18,14 @@ __device__ __forceinline__ double resolve_entry(const MsgParams& mp, uint32_t st
     return xj;
 }
 
+// DESIGN.md §9 bounded delay: sender j's value as delivered on slot s in round r, given the
+// slot's DELAY draw w: x_j^{r - min(r, w mod (D + 1))}.
+__device__ __forceinline__ double delayed_x(const RoundArgs& a, uint32_t lb, uint32_t r, uint32_t w, uint64_t j) {
+    uint32_t dl = w % (a.delay + 1);
+    dl = dl < r ? dl : r;
+    return a.xh[(uint64_t)((r - dl) % a.H) * a.xstride + (uint64_t)lb * a.N + j];
+}
+
 __device__ __forceinline__ double wave_min(double v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v = __builtin_fmin(v, __shfl_xor(v, o, 64));

@@ -97,7 +97,8 @@ __global__ __launch_bounds__(kGenericBlock) void k_round_generic(const RoundArgs
             } else {
                 const uint32_t stj = stv ? stv[j] : kHonest;
                 const bool dropped = mp.thr && draw(mp.key, kStreamDrop, bG, r, slot) < mp.thr;
-                v = resolve_entry(mp, stj, x[j], xi, dropped, b, r, i, slot, lo, hi);
+                const double xj = a.delay ? delayed_x(a, lb, r, draw(mp.key, kStreamDelay, b, r, slot), j) : x[j];
+                v = resolve_entry(mp, stj, xj, xi, dropped, b, r, i, slot, lo, hi);
             }
         }
         sh[e] = v;

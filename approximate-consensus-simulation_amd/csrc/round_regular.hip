@@ -72,7 +72,18 @@ __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs
                 double xj[D];
                 uint32_t sj[D];
                 // all gathers first, unconditionally (the branch is uniform and hoisted)
-                if (stv) {
+                if (a.delay) {   // bounded delay: one DELAY Philox call per 4 slots, history gathers
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        const U4 wd = philox10(i * (uint32_t)NQ + q, r, b, kStreamDelay, mp.key);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const int t = 4 * q + e;
+                            xj[t] = delayed_x(a, lb, r, wd.v[e], col[t]);
+                            sj[t] = stv ? stv[col[t]] : kHonest;
+                        }
+                    }
+                } else if (stv) {
 #pragma unroll
                     for (int t = 0; t < D; ++t) {
                         xj[t] = x[col[t]];

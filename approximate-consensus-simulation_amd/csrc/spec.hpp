@@ -15,6 +15,7 @@ namespace acs {
 
 constexpr uint32_t kHonest = 0xFFFFFFFFu;     // §A.4 status word: honest
 constexpr uint32_t kByz = 0xFFFFFFFEu;        // §A.4 status word: Byzantine (else: crash round)
+constexpr uint32_t kStreamDelay = 7;   // bounded-delay rounds
 constexpr uint32_t kStreamInit = 0, kStreamDrop = 1, kStreamFaultset = 2, kStreamCrashRound = 3,
                    kStreamCrashPartial = 4, kStreamByz = 5, kStreamGraph = 6;
 

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define ACS_ABI_VERSION 1
+#define ACS_ABI_VERSION 2   /* 2: acs_config.delay_max (bounded-delay rounds) */
 
 /* status codes */
 #define ACS_OK            0
@@ -81,6 +81,7 @@ extern "C" {
 #define ACS_STREAM_CRASH_PARTIAL 4u
 #define ACS_STREAM_BYZ           5u
 #define ACS_STREAM_GRAPH         6u
+#define ACS_STREAM_DELAY         7u   /* bounded-delay rounds */
 
 /* Opaque simulation handle. */
 typedef struct acs_sim acs_sim;
@@ -111,6 +112,8 @@ typedef struct acs_config {
     uint32_t trace_spread;     /* 1: keep spread^r for every round (per instance) */
     uint32_t omp_threads;      /* CPU oracle only; ignored by the HIP library */
     uint64_t instance_offset;  /* global id of local instance 0 (multi-GPU instance sharding, §8e) */
+    uint32_t delay_max;        /* D: bounded-delay rounds; 0 = synchronous (§A.6) */
+    uint32_t reserved0;        /* must be 0 */
 } acs_config;
 
 /* Result of acs_round. For B > 1: round = max rounds over instances,

@@ -247,6 +247,8 @@ int acso_validate(const acs_config* c) {
     if (!(c->eps >= 0.0 && c->eps <= 1e300)) return fail(ACS_EINVAL, "eps must be finite, >= 0");
     if (c->termination > ACS_TERM_FIXED) return fail(ACS_EINVAL, "unknown termination");
     if (c->dtype != ACS_F64) return fail(ACS_EUNSUPPORTED, "only ACS_F64 is implemented");
+    if (c->delay_max > 64) return fail(ACS_EINVAL, "delay_max must be <= 64");
+    if (c->reserved0 != 0) return fail(ACS_EINVAL, "reserved0 must be 0");
     if (c->trace_spread && c->n_instances * ((uint64_t)c->max_rounds + 1) > (1ull << 28))
         return fail(ACS_EINVAL, "spread trace too large (B*(max_rounds+1) > 2^28)");
     return ACS_OK;
@@ -264,6 +266,7 @@ struct acso_sim {
     uint32_t* status;        /* B*N: HONEST / BYZ / crash round (§A.4) */
     double* x;               /* B*N current values */
     double* xn;              /* B*N next values */
+    double* hist;            /* (D+1)*B*N: x^q in slot q % (D+1) for the last D+1 rounds (delay_max D > 0) */
     uint32_t* rounds;        /* B */
     uint8_t* done;           /* B */
     uint8_t* converged;      /* B */
@@ -329,8 +332,9 @@ int acso_create(const acs_config* cfg, acso_sim** out) {
         s->trace = (double*)malloc(nt * sizeof(double));
         if (s->trace) for (uint64_t k = 0; k < nt; ++k) s->trace[k] = NAN;
     }
+    if (cfg->delay_max) s->hist = (double*)malloc(((uint64_t)cfg->delay_max + 1) * BN * sizeof(double));
     if (!s->status || !s->x || !s->xn || !s->rounds || !s->done || !s->converged || !s->lo ||
-        !s->hi || (cfg->trace_spread && !s->trace)) {
+        !s->hi || (cfg->trace_spread && !s->trace) || (cfg->delay_max && !s->hist)) {
         acso_destroy(s);
         return fail(ACS_ENOMEM, "oom");
     }
@@ -372,6 +376,7 @@ int acso_create(const acs_config* cfg, acso_sim** out) {
         }
         s->rounds[lb] = 0;
         after_update(s, lb);
+        if (s->hist) memcpy(s->hist + lb * s->N, x, s->N * sizeof(double));   /* x^0 in slot 0 */
     }
     *out = s;
     return ACS_OK;
@@ -430,7 +435,7 @@ int acso_create_csr(const acs_config* cfg, const uint64_t* rowptr, const uint32_
 void acso_destroy(acso_sim* s) {
     if (!s) return;
     free(s->rowptr); free(s->colidx);
-    free(s->nbr); free(s->status); free(s->x); free(s->xn); free(s->rounds); free(s->done);
+    free(s->nbr); free(s->status); free(s->x); free(s->xn); free(s->hist); free(s->rounds); free(s->done);
     free(s->converged); free(s->lo); free(s->hi); free(s->trace);
     free(s);
 }
@@ -447,6 +452,15 @@ static double byz_value(const acso_sim* s, uint32_t b, uint32_t r, uint64_t i, u
     return (lo - c->byz_delta) + u * width;
 }
 
+/* the delivered value of sender j on slot `slot` in round r is x_j^{r - delta} with
+ * delta = min(r, draw(DELAY, b, r, slot) mod (D + 1)); D = 0 is the synchronous §A.6 model. */
+static double delayed_value(const acso_sim* s, uint64_t lb, uint32_t b, uint32_t r, uint64_t j, uint64_t slot) {
+    const uint32_t D = s->c.delay_max;
+    uint32_t delta = acso_draw(s->c.seed, ACS_STREAM_DELAY, b, r, slot) % (D + 1);
+    if (delta > r) delta = r;
+    return s->hist[((uint64_t)((r - delta) % (D + 1)) * s->B + lb) * s->N + j];
+}
+
 /* §A.6: resolve entry (i <- j, slot, round r) for an active receiver i != j-as-self. */
 static double resolve(const acso_sim* s, uint32_t b, uint32_t bG, uint32_t r, const double* x,
                       const uint32_t* st, uint64_t i, uint64_t j, uint64_t slot, double lo, double hi) {
@@ -460,6 +474,7 @@ static double resolve(const acso_sim* s, uint32_t b, uint32_t bG, uint32_t r, co
         missing = acso_draw(s->c.seed, ACS_STREAM_DROP, bG, r, slot) < s->thr;
     if (missing) return x[i];
     if (sj == BYZ) return byz_value(s, b, r, i, slot, lo, hi);
+    if (s->c.delay_max) return delayed_value(s, (uint64_t)(b - (uint32_t)s->c.instance_offset), b, r, j, slot);
     return x[j];
 }
 
@@ -505,8 +520,10 @@ static void step_instance(acso_sim* s, uint64_t lb) {
         }
         free(S);
     }
-    /* swap x / xn for this instance */
+    /* swap x / xn for this instance; keep x^{r+1} in the delay history */
     memcpy(s->x + lb * N, xn, N * sizeof(double));
+    if (s->hist)
+        memcpy(s->hist + ((uint64_t)((r + 1) % (c->delay_max + 1)) * s->B + lb) * N, xn, N * sizeof(double));
     s->rounds[lb] = r + 1;
     after_update(s, lb);
 }
@@ -600,6 +617,9 @@ int acso_set_state(acso_sim* s, uint32_t round, const double* x, uint64_t n) {
     if (!s || !x || n != s->B * s->N) return fail(ACS_EINVAL, "set_state needs B*N values");
     if (round > s->c.max_rounds) return fail(ACS_EINVAL, "round > max_rounds");
     memcpy(s->x, x, n * sizeof(double));
+    /* bounded-delay history restarts from x: every past slot holds x^round */
+    if (s->hist)
+        for (uint64_t q = 0; q <= s->c.delay_max; ++q) memcpy(s->hist + q * n, x, n * sizeof(double));
     for (uint64_t b = 0; b < s->B; ++b) {
         s->rounds[b] = round;
         after_update(s, b);

@@ -15,7 +15,7 @@ W0, W1 = np.uint64(0x9E3779B9), np.uint64(0xBB67AE85)
 HONEST = 0xFFFFFFFF
 BYZ = 0xFFFFFFFE
 
-INIT, DROP, FAULTSET, CRASH_ROUND, CRASH_PARTIAL, BYZS, GRAPH = range(7)
+INIT, DROP, FAULTSET, CRASH_ROUND, CRASH_PARTIAL, BYZS, GRAPH, DELAY = range(8)
 
 
 def philox(c0, c1, c2, c3, k0, k1):
@@ -180,6 +180,9 @@ class NpSim:
                     cr = draw(self.seed, CRASH_ROUND, b, 0, fv.astype(np.uint64)).astype(np.uint64)
                     self.status[lb, fv] = cr % np.uint64(cfg.crash_window)
         self.rounds = np.zeros(self.B, dtype=np.int64)
+        # bounded-delay rounds: every past x^q, q = 0..r
+        self.D = int(getattr(cfg, "delay_max", 0))
+        self.hist = [[self.x[lb].copy()] for lb in range(self.B)]
         self.trace = [[] for _ in range(self.B)]
         self.lo = np.zeros(self.B)
         self.hi = np.zeros(self.B)
@@ -237,6 +240,7 @@ class NpSim:
             V = self._values(A, J, slots, selfm, r, b, bG, x, st, lo, hi)
             xn[A] = apply_rule(self.rule, self.t, V, x[A])
         self.x[lb] = xn
+        self.hist[lb].append(xn.copy())
         self.rounds[lb] = r + 1
         self._after(lb)
 
@@ -254,6 +258,15 @@ class NpSim:
                 cand = ~missing & ~selfm
                 missing[cand] = draw(self.seed, DROP, bG, r, slots[cand]) < np.uint32(self.thr)
             V = x[J].copy()
+            if self.D:
+                # delivered value x_j^{r - delta}, delta = min(r, draw(DELAY, b, r, s) mod (D + 1))
+                lb = b - int(cfg.instance_offset)
+                dl = (draw(self.seed, DELAY, b, r, slots) % np.uint32(self.D + 1)).astype(np.int64)
+                dl = np.minimum(dl, r)
+                for dv in range(1, self.D + 1):
+                    mk = (dl == dv) & ~selfm
+                    if mk.any():
+                        V[mk] = self.hist[lb][r - dv][J[mk]]
             byzm = (sj == BYZ) & ~selfm & ~missing
             if byzm.any():
                 d = float(cfg.byz_delta)

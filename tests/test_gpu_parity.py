@@ -104,6 +104,20 @@ CASES = {
     "wmsr_batched40_crash_drop": Config(n_nodes=40, n_instances=20, topology="complete", rule="wmsr",
                                         trim=6, fault_model="crash", n_faulty=5, crash_window=4,
                                         loss_p=0.2, eps=1e-10, max_rounds=300, seed=55, trace_spread=True),
+    # bounded-delay rounds: per-lane regular kernel and the generic kernel
+    "delay4_reg16_t5_clean": Config(n_nodes=40000, topology="regular", degree=16, rule="trimmed", trim=5,
+                                    delay_max=4, eps=1e-9, max_rounds=300, seed=61, trace_spread=True),
+    "delay2_reg32_t5_byz_drop": Config(n_nodes=20000, topology="regular", degree=32, rule="trimmed", trim=5,
+                                       fault_model="byzantine", n_faulty=400, byz_strategy="random",
+                                       byz_delta=0.1, loss_p=0.1, delay_max=2, eps=1e-8, max_rounds=300,
+                                       seed=62, trace_spread=True),
+    "delay3_complete60_avg_batched_shape": Config(n_nodes=60, n_instances=6, topology="complete",
+                                                  rule="average", loss_p=0.2, delay_max=3, eps=1e-10,
+                                                  max_rounds=400, seed=63, trace_spread=True),
+    "delay1_complete300_split": Config(n_nodes=300, topology="complete", rule="midpoint", trim=50,
+                                       fault_model="byzantine", n_faulty=50, byz_strategy="split",
+                                       byz_delta=0.05, delay_max=1, eps=1e-9, max_rounds=500, seed=64,
+                                       trace_spread=True),
     # generic kernel (odd d / t, dense complete graphs)
     "generic_reg10_t3": Config(n_nodes=7000, topology="regular", degree=10, rule="trimmed", trim=3,
                                fault_model="crash", n_faulty=100, crash_window=6, loss_p=0.05,
@@ -253,3 +267,19 @@ def test_dense_persistent_multi_instance(oracle_mod):
         assert g.kernel_name() == "k_dense_persist"
     g, o = run_both(oracle_mod, cfg)
     assert_same(g, o)
+
+
+def test_delay_resume_matches_oracle(oracle_mod):
+    """set_state with delays restarts the history from x on both sides."""
+    cfg = CASES["delay4_reg16_t5_clean"]
+    with acsim.Simulator(cfg, device=0) as g, oracle_mod.OracleSimulator(cfg, threads=8) as o:
+        g.round(6)
+        o.round(6)
+        mid = g.values(0).copy()
+        assert np.array_equal(bits(mid), bits(o.values(0)))
+        g.set_state(3, mid[None, :])
+        o.set_state(3, mid[None, :])
+        g.run()
+        o.run()
+        assert np.array_equal(g.rounds(), o.rounds())
+        assert np.array_equal(bits(g.values(0)), bits(o.values(0)))

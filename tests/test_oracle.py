@@ -120,8 +120,15 @@ def test_oracle_reproduces_golden(oracle_mod, name):
            seed=13, trace_spread=True),
     Config(n_nodes=40, topology="complete", rule="wmsr", trim=6, fault_model="crash", n_faulty=5,
            crash_window=4, eps=1e-10, max_rounds=300, seed=14, trace_spread=True),
+    Config(n_nodes=300, topology="regular", degree=8, rule="trimmed", trim=2, fault_model="byzantine",
+           n_faulty=10, byz_strategy="split", byz_delta=0.1, loss_p=0.05, delay_max=3, eps=1e-9,
+           max_rounds=300, seed=16, trace_spread=True),
+    Config(n_nodes=30, n_instances=3, topology="complete", rule="average", fault_model="crash", n_faulty=3,
+           crash_window=5, delay_max=2, eps=1e-10, max_rounds=300, seed=17, instance_offset=4,
+           trace_spread=True),
 ], ids=["complete_mid_crash_drop", "regular_dlpsw_split", "batched_avg_fixed_grouped",
-        "regular_wmsr_byzrandom_drop", "complete_wmsr_crash"])
+        "regular_wmsr_byzrandom_drop", "complete_wmsr_crash", "regular_delay3_split_drop",
+        "complete_avg_delay2_crash"])
 def test_oracle_matches_numpy(oracle_mod, cfg):
     with oracle_mod.OracleSimulator(cfg) as o:
         o.run()
