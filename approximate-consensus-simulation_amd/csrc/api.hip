@@ -335,7 +335,7 @@ static int enqueue_round(acs_sim* s, uint32_t r) {
     if (rc) return rc;
     if (!s->partitioned) {
         if (s->binned) {
-            HIP_TRY(launch_round_binned(s->bin, a, s->stream));
+            HIP_TRY(launch_round_binned(s->bin, a, s->clean, s->stream));
         } else if (s->path == PATH_REGULAR) {
             HIP_TRY(launch_round_regular(a, s->B, s->clean, s->stream));
         } else if (s->path == PATH_DENSE) {
@@ -380,7 +380,7 @@ static int enqueue_round(acs_sim* s, uint32_t r) {
             ap.partial = s->partial + (uint64_t)p * s->nblk;
             if (ap.nrows == 0) continue;   // empty tail partition (its partials are not folded)
             if (s->binned)
-                HIP_TRY(launch_round_binned(p == 0 ? s->bin : s->parts[p - 1].bin, ap, s->stream));
+                HIP_TRY(launch_round_binned(p == 0 ? s->bin : s->parts[p - 1].bin, ap, s->clean, s->stream));
             else
                 HIP_TRY(launch_round_regular(ap, s->B, s->clean, s->stream));
         }
@@ -408,7 +408,7 @@ static int enqueue_round(acs_sim* s, uint32_t r) {
     a.nrows = part_rows(s, s->rank);
     if (a.nrows) {
         if (s->binned)
-            HIP_TRY(launch_round_binned(s->bin, a, s->stream));
+            HIP_TRY(launch_round_binned(s->bin, a, s->clean, s->stream));
         else
             HIP_TRY(launch_round_regular(a, s->B, s->clean, s->stream));
     }
@@ -623,9 +623,10 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     }
     s->ell_sorted = s->path == PATH_REGULAR && s->clean && cfg->rule != ACS_RULE_AVERAGE;
     const uint64_t rows_local = partitioned ? s->rows_per : s->N;
-    // binned exchange (round_binned.hip): clean, order-independent rule, one instance, and a graph
-    // shape with one or two exchange levels; ACSIM_BINNED=0 forces the per-lane kernel and
-    // ACSIM_BIN_SA sets the source block size (tests use small blocks on small graphs)
+    // binned exchange (round_binned.hip): one instance, synchronous rounds, and a graph shape with
+    // one or two exchange levels (faults and loss are resolved in phase B from tagged values and
+    // slot-order draws); ACSIM_BINNED=0 forces the per-lane kernel and ACSIM_BIN_SA sets the
+    // source block size (tests use small blocks on small graphs)
     uint32_t bin_sa = 16384;
     if (const char* v = getenv("ACSIM_BIN_SA")) bin_sa = (uint32_t)strtoul(v, nullptr, 10);
     if (bin_sa < 64 || bin_sa > 16384 || (bin_sa & (bin_sa - 1))) bin_sa = 16384;
@@ -633,12 +634,12 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         const char* env = getenv("ACSIM_BINNED");
         const bool allow = !(env && env[0] == '0');
         const uint32_t lv = s->path == PATH_REGULAR && s->d ? binned_levels(s->N, rows_local, s->d, bin_sa, nullptr) : 0;
-        s->binned = allow && s->path == PATH_REGULAR && s->clean && s->B == 1 && lv != 0 &&
+        s->binned = allow && s->path == PATH_REGULAR && cfg->delay_max == 0 && s->B == 1 && lv != 0 &&
                     binned_supported(s->d, cfg->trim, cfg->rule) && rows_local * s->d < (1ull << 32);
         if (s->binned) {
             char nm[96];
-            snprintf(nm, sizeof nm, "k_bin_scatter+%sk_bin_gather<%u,%u>", lv == 2 ? "k_bin_regroup+" : "", s->d,
-                     cfg->trim);
+            snprintf(nm, sizeof nm, "k_bin_scatter+%sk_bin_gather<%u,%u%s>%s", lv == 2 ? "k_bin_regroup+" : "", s->d,
+                     cfg->trim, s->clean ? "" : ",faulty", cfg->fault_model != ACS_FAULT_NONE ? "+k_bin_tag" : "");
             s->kname = nm;
         }
     }
@@ -686,6 +687,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         CREATE_TRY(hipMalloc(&s->trace, nt * sizeof(double)));
         CREATE_TRY(hipMemsetAsync(s->trace, 0xFF, nt * sizeof(double), s->stream));   // NaN
     }
+    const bool tagged = cfg->fault_model != ACS_FAULT_NONE;
     if (cfg->topology == ACS_TOPO_RANDOM_REGULAR) {
         const uint64_t words = ((rows_local + 63) / 64) * 64ull * s->dp;
         CREATE_TRY(hipMalloc(&s->ell, words * sizeof(uint32_t)));
@@ -693,7 +695,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         CREATE_TRY(build_rows(s, s->ell, partitioned ? rank : 0));
         if (s->binned) {   // the plan replaces the ELL in the round loop
             const uint64_t nr = partitioned ? part_rows(s, rank) : s->N;
-            if (nr) CREATE_TRY(binned_build(s->bin, s->ell, s->N, nr, s->d, s->dp, bin_sa, s->stream));
+            if (nr) CREATE_TRY(binned_build(s->bin, s->ell, s->N, nr, s->d, s->dp, bin_sa, tagged, s->stream));
             (void)hipFree(s->ell);
             s->ell = nullptr;
         }
@@ -708,7 +710,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
                 CREATE_TRY(build_rows(s, q.ell, p));
                 if (s->binned) {
                     const uint64_t nr = part_rows(s, p);
-                    if (nr) CREATE_TRY(binned_build(q.bin, q.ell, s->N, nr, s->d, s->dp, bin_sa, s->stream));
+                    if (nr) CREATE_TRY(binned_build(q.bin, q.ell, s->N, nr, s->d, s->dp, bin_sa, tagged, s->stream));
                     (void)hipFree(q.ell);
                     q.ell = nullptr;
                 }

@@ -104,8 +104,8 @@ const char* regular_fast_name(uint32_t d, uint32_t t, bool clean);
 hipError_t launch_round_regular(const RoundArgs& a, uint64_t B, bool clean, hipStream_t s);
 constexpr uint32_t kRegularBlock = 256;
 
-// Binned exchange (round_binned.hip): the clean, order-independent RANDOM_REGULAR round as
-// streaming kernels instead of N·d random 8-byte gathers.  Deliveries (i <- j) are grouped into
+// Binned exchange (round_binned.hip): the one-instance RANDOM_REGULAR round as streaming kernels
+// instead of N·d random 8-byte gathers (clean, lossy and faulty configs; no delays).  Deliveries (i <- j) are grouped into
 // tiles of (source block of SA senders, receiver group) and stored with tiles padded to even
 // lengths.  Phase A (an LDS-resident source block per workgroup) streams stage1[p] = x[src(p)];
 // for two-level plans phase M regroups stage1 by receiver block into stage2; phase B (one
@@ -126,15 +126,18 @@ struct BinnedPlan {
     uint64_t* moff = nullptr;           // [ngroups+1] stage2 start of phase-M group g
     double* stage1 = nullptr;           // [Ep1]
     double* stage2 = nullptr;           // [Ep2] (two levels)
+    double* xtag = nullptr;             // [N+2] tagged sender values (fault schedules only)
 };
 bool binned_supported(uint32_t d, uint32_t t, uint32_t rule);
 // 1 or 2 exchange levels for NR local receivers of an N-node graph (0: not supported).
 uint32_t binned_levels(uint64_t N, uint64_t NR, uint32_t d, uint32_t sa, uint32_t* sr_out);
-// Builds the plan from the ELL of the NR local rows (sorted or spec order); sa = source block size.
+// Builds the plan from the ELL of the NR local rows (sorted or spec order; slot-dependent configs
+// need spec order); sa = source block size; tagged: the config has a fault schedule.
 hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t NR, uint32_t d, uint32_t dp,
-                        uint32_t sa, hipStream_t s);
+                        uint32_t sa, bool tagged, hipStream_t s);
 void binned_free(BinnedPlan& p);
-hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, hipStream_t s);
+// clean: no slot-dependent decision (selects the plain phase-B instantiation)
+hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool clean, hipStream_t s);
 
 // Generic kernel: one workgroup per receiver, LDS bitonic sort (any topology, m <= 8192).
 constexpr uint32_t kGenericMaxM = 8192;

@@ -18,9 +18,19 @@
 //            invpos (LDS), the §A.7 rule in registers (rules.hpp), one store, block (min, max)
 //            partial.                                                  8 B + 2 B read / delivery
 //
-// Only clean configs with an order-independent rule (TRIMMED / MIDPOINT / DLPSW) take this path:
-// the rule depends on the multiset of received values only, so the slot a value lands in does
-// not matter and the result is bit-identical to the spec (same sorted sequence, same §A.7 sum).
+// invpos is indexed by ELL slot t, so phase B sees receiver i's values in slot order: with the
+// ELL in spec order (every config but the clean sort-based ones, whose rows are stored sorted)
+// slot t is the spec slot s = i·d + t and the §A.5 drop draws, §A.4 crash draws and AVERAGE's
+// entry-order sum all follow the spec exactly.
+//
+// Fault schedules (§A.4): phase B needs each delivered value's sender status.  Instead of a
+// second exchange of status words, k_bin_tag rewrites x into xtag once per round: a sender that
+// is Byzantine, crashing this round (partial) or crashed earlier (silent) is replaced by a quiet
+// NaN whose payload holds that mode (x is never NaN, validated); phase A streams xtag instead of
+// x, and phase B decodes the tag to the sender's §A.6 resolution.  A partial sender's message
+// still delivers x_j when its per-slot draw passes, so its tag also carries j and phase B
+// fetches x_j itself (n_faulty / crash_window senders per round at most).  +12 B read, +8 B
+// written per node per round, against the 8·d B of random gathers the per-lane kernel spends.
 #include <hipcub/hipcub.hpp>
 
 #include <vector>
@@ -134,7 +144,27 @@ __global__ __launch_bounds__(kBinA) void k_bin_regroup(const double* __restrict_
 // ------------------------------------------------------------------------------ phase B
 // The runs of block b (run j of a table row of nrun + 1 descriptors) are copied into LDS,
 // concatenated; lane i_local then reads its D values at invpos[b][t][i_local].
-template <int D, int T, bool WMSR = false>
+// quiet-NaN tag of a non-normal sender: payload bits 0-1 = 1 Byzantine, 2 crashing this round,
+// 3 silent; bits 2-33 = the sender id (read back for mode 2; B·N < 2^31 with a fault schedule)
+constexpr uint64_t kTagBase = 0x7FF8000000000000ull;
+
+__global__ __launch_bounds__(256) void k_bin_tag(const double* __restrict__ x, const uint32_t* __restrict__ status,
+                                                 double* __restrict__ xt, uint64_t N, uint32_t r,
+                                                 const InstState* __restrict__ st) {
+    if (st->done) return;
+    const uint64_t j = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 2;
+    if (j >= N) return;
+    const uint32_t n = N - j >= 2 ? 2u : 1u;
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) {
+        if (k >= n) break;
+        const uint32_t sj = status[j + k];
+        const uint64_t mode = sj == kHonest ? 0 : sj == kByz ? 1 : r < sj ? 0 : r == sj ? 2 : 3;
+        xt[j + k] = mode ? __longlong_as_double((long long)(kTagBase | (j + k) << 2 | mode)) : x[j + k];
+    }
+}
+
+template <int D, int T, bool WMSR = false, bool FAULTY = false>
 __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const double* __restrict__ stage,
                                                        const uint16_t* __restrict__ invpos,
                                                        const uint2* __restrict__ tiles, uint32_t nrun, uint32_t Q,
@@ -158,6 +188,10 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
     const bool live = li < a.nrows;
     // ordinary loads first (their wait is the barrier's vmcnt(0) anyway)
     const double xi = live ? a.xin[i] : 0.0;
+    uint32_t si = kHonest;
+    if constexpr (FAULTY) {
+        if (a.status && live) si = a.status[i];
+    }
     uint4 ip[D / 8];
     const uint4* ipp = reinterpret_cast<const uint4*>(invpos) + (uint64_t)b * (D / 8) * kBinSB + threadIdx.x;
 #pragma unroll
@@ -167,21 +201,52 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
 
     double mn = kInf, mx = -kInf;
     if (live) {
-        double v[D + 1];
-        v[0] = xi;
+        double res = xi;
+        if (!FAULTY || is_active(si, a.r)) {
+            double v[D + 1];
+            v[0] = xi;
 #pragma unroll
-        for (int q = 0; q < D / 8; ++q) {
-            const uint32_t wd[4] = {ip[q].x, ip[q].y, ip[q].z, ip[q].w};
+            for (int q = 0; q < D / 8; ++q) {
+                const uint32_t wd[4] = {ip[q].x, ip[q].y, ip[q].z, ip[q].w};
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                v[1 + 8 * q + 2 * e] = raw[wd[e] & 0xFFFFu];
-                v[2 + 8 * q + 2 * e] = raw[wd[e] >> 16];
+                for (int e = 0; e < 4; ++e) {
+                    v[1 + 8 * q + 2 * e] = raw[wd[e] & 0xFFFFu];
+                    v[2 + 8 * q + 2 * e] = raw[wd[e] >> 16];
+                }
             }
+            if constexpr (FAULTY) {   // §A.5 drops, §A.4 / §A.6 sender resolution (round_regular.hip order)
+                const MsgParams& mp = a.mp;
+                const uint32_t bI = (uint32_t)mp.inst_offset, bG = bI - bI % mp.mask_group;
+                const uint32_t r = a.r, iu = (uint32_t)i;
+                const double lo = S->lo, hi = S->hi;
+#pragma unroll
+                for (int q = 0; q < D / 4; ++q) {
+                    U4 w;
+                    w.v[0] = w.v[1] = w.v[2] = w.v[3] = 0xFFFFFFFFu;
+                    if (mp.thr) w = philox10(iu * (uint32_t)(D / 4) + q, r, bG, kStreamDrop, mp.key);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int t = 4 * q + e;
+                        double u = v[1 + t];
+                        const uint64_t bits = (uint64_t)__double_as_longlong(u);
+                        uint32_t stj = kHonest;
+                        if ((bits >> 51) == 0xFFFull) {
+                            const uint32_t md = (uint32_t)(bits & 3u);
+                            stj = md == 1 ? kByz : md == 2 ? r : r - 1;   // silent implies r >= 1
+                            if (md == 2) u = a.xin[(bits >> 2) & 0xFFFFFFFFull];
+                        }
+                        v[1 + t] = resolve_entry(mp, stj, u, xi, w.v[e] < mp.thr, bI, r, iu, (uint64_t)iu * D + t,
+                                                 lo, hi);
+                    }
+                }
+            }
+            res = apply_rule_reg<D, T, WMSR>(a.rule, v);
         }
-        const double res = apply_rule_reg<D, T, WMSR>(a.rule, v);
         a.xout[i] = res;
-        mn = res;
-        mx = res;
+        if (si == kHonest) {
+            mn = res;
+            mx = res;
+        }
     }
     block_minmax_store<kBinSB>(mn, mx, a.partial + b);
 }
@@ -346,7 +411,8 @@ __global__ __launch_bounds__(256) void k_bin_inv(uint64_t E, BinGeom G, uint32_t
 #define ACS_BINNED_VARIANTS(X) X(16, 5) X(32, 5) X(16, 0) X(32, 0) X(8, 2) X(8, 0)
 
 bool binned_supported(uint32_t d, uint32_t t, uint32_t rule) {
-    if (rule < 1 || rule > 4) return false;   // sort-based rules only (W-MSR also reads x_i, which phase B has)
+    if (rule > 4) return false;
+    if (rule == 0 && t != 0) return false;   // AVERAGE: entry order (the rows must be in spec order)
     if (rule == 3 && t < 1) return false;
 #define X(DD, TT) if (d == DD && t == TT) return true;
     ACS_BINNED_VARIANTS(X)
@@ -381,6 +447,7 @@ void binned_free(BinnedPlan& p) {
     (void)hipFree(p.moff);
     (void)hipFree(p.stage1);
     (void)hipFree(p.stage2);
+    (void)hipFree(p.xtag);
     p = BinnedPlan{};
 }
 
@@ -451,7 +518,7 @@ hipError_t tile_sort(const uint32_t* ell, uint64_t E, const BinGeom& G, int leve
 }  // namespace
 
 hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t NR, uint32_t d, uint32_t dp,
-                        uint32_t sa, hipStream_t s) {
+                        uint32_t sa, bool tagged, hipStream_t s) {
     hipError_t e = hipSuccess;
     uint32_t sr = 0;
     const uint32_t levels = binned_levels(N, NR, d, sa, &sr);
@@ -497,6 +564,7 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     if (e == hipSuccess) e = hipMemsetAsync(p.idxA, 0, p.Ep1 * 2, s);
     if (e == hipSuccess) e = hipMalloc(&p.stage1, p.Ep1 * sizeof(double));
     if (e == hipSuccess) e = hipMalloc(&p.aoff, ((uint64_t)G.P + 1) * sizeof(uint64_t));
+    if (e == hipSuccess && tagged) e = hipMalloc(&p.xtag, (N + 2) * sizeof(double));
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_bin_fill_a, dim3(grid), dim3(256), 0, s, ell, E, G, T1.ks, T1.vs, T1.tl, T1.pstart, p.idxA);
         hipLaunchKernelGGL(k_bin_aoff, dim3((G.P + 256) / 256), dim3(256), 0, s, T1.pstart, G.P, G.R, p.Ep1, p.aoff);
@@ -575,7 +643,7 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     return e;
 }
 
-hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, hipStream_t s) {
+hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool clean, hipStream_t s) {
     static bool attr = false;   // source blocks above 8192 senders / phase-M images need > 64 KiB of LDS
     if (!attr) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_scatter),
@@ -586,7 +654,14 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, hipStrea
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL(k_bin_scatter, dim3(p.P * p.segs), dim3(kBinA), p.SA * sizeof(double), s, a.xin, p.idxA, p.aoff,
+    const double* src = a.xin;
+    if (!clean && a.status) {
+        if (!p.xtag) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_bin_tag, dim3((unsigned)((a.N + 511) / 512)), dim3(256), 0, s, a.xin, a.status, p.xtag,
+                           a.N, a.r, a.st);
+        src = p.xtag;
+    }
+    hipLaunchKernelGGL(k_bin_scatter, dim3(p.P * p.segs), dim3(kBinA), p.SA * sizeof(double), s, src, p.idxA, p.aoff,
                        p.stage1, a.st, a.N, p.SA, p.segs, p.chunk);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -602,12 +677,19 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, hipStrea
     const dim3 grid(8 * Qc);
 #define X(DD, TT)                                                                                        \
     if (p.D == DD && a.trim == TT) {                                                                     \
-        if (a.rule == 4)                                                                                 \
+        const bool w_ = a.rule == 4;                                                                     \
+        if (clean && w_)                                                                                 \
             hipLaunchKernelGGL((k_bin_gather<DD, TT, true>), grid, dim3(kBinSB), 0, s, a, last, p.invpos,   \
                                p.tiles, p.nrun, p.Q, Qc);                                                \
-        else                                                                                             \
+        else if (clean)                                                                                  \
             hipLaunchKernelGGL((k_bin_gather<DD, TT>), grid, dim3(kBinSB), 0, s, a, last, p.invpos, p.tiles, \
                                p.nrun, p.Q, Qc);                                                         \
+        else if (w_)                                                                                     \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, true, true>), grid, dim3(kBinSB), 0, s, a, last,       \
+                               p.invpos, p.tiles, p.nrun, p.Q, Qc);                                      \
+        else                                                                                             \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, false, true>), grid, dim3(kBinSB), 0, s, a, last,      \
+                               p.invpos, p.tiles, p.nrun, p.Q, Qc);                                      \
         return hipGetLastError();                                                                        \
     }
     ACS_BINNED_VARIANTS(X)

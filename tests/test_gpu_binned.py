@@ -1,8 +1,9 @@
 """Binned-exchange round (csrc/round_binned.hip) against the CPU oracle and the per-lane kernel.
 
-The binned path serves clean RANDOM_REGULAR configs with a sort-based rule (TRIMMED / MIDPOINT /
-DLPSW) on one instance.  Bar: bit-exact final values, spread traces and rounds (the rule depends
-only on the multiset of received values, so the slot a value lands in cannot change the result).
+The binned path serves one-instance RANDOM_REGULAR configs with synchronous rounds: clean ones
+with any rule, and lossy / crash / Byzantine ones, whose per-slot decisions phase B makes from the
+slot-ordered values and the tag k_bin_tag puts on non-normal senders.  Bar: bit-exact final
+values, spread traces and rounds against the oracle and the per-lane kernel.
 ACSIM_BIN_SA shrinks the source block so that small graphs still span many blocks and ragged
 last blocks, and (below a mean of 64 deliveries per (source block, receiver block) tile) take the
 two-level plan with the phase-M regroup; ACSIM_BINNED=0 forces the per-lane kernel for the
@@ -61,6 +62,31 @@ CASES = {
     "d32_t5_dlpsw_sa2048": (Config(n_nodes=40000, topology="regular", degree=32, rule="dlpsw", trim=5,
                                    eps=1e-10, max_rounds=300, seed=7, trace_spread=True), 2048),
     "cfg4_shape_2e17": (preset("cfg4_eps", n_nodes=1 << 17, trace_spread=True), 8192),
+    "d32_avg_clean_sa1024": (Config(n_nodes=30000, topology="regular", degree=32, rule="average", eps=1e-10,
+                                    max_rounds=300, seed=41, trace_spread=True), 1024),
+    # slot-dependent configs: loss, crash (partial + silent rounds), Byzantine strategies
+    "faulty_d32_t5_byzrandom_drop_sa1024": (Config(n_nodes=50000, topology="regular", degree=32, rule="trimmed",
+                                                   trim=5, fault_model="byzantine", n_faulty=1500,
+                                                   byz_strategy="random", byz_delta=0.2, loss_p=0.1, eps=1e-8,
+                                                   max_rounds=300, seed=42, trace_spread=True), 1024),
+    "faulty_two_level_d16_t5_crash_drop_sa256": (Config(n_nodes=100000, topology="regular", degree=16,
+                                                        rule="trimmed", trim=5, fault_model="crash",
+                                                        n_faulty=3000, crash_window=6, loss_p=0.15, eps=1e-8,
+                                                        max_rounds=300, seed=43, trace_spread=True), 256),
+    "faulty_d16_avg_drop_sa512": (Config(n_nodes=40000, topology="regular", degree=16, rule="average",
+                                         loss_p=0.2, eps=1e-9, max_rounds=300, seed=44, trace_spread=True), 512),
+    "faulty_d8_mid_byzconst_sa256": (Config(n_nodes=30001, topology="regular", degree=8, rule="midpoint", trim=2,
+                                            fault_model="byzantine", n_faulty=300, byz_strategy="constant",
+                                            byz_const=-3.0, eps=1e-7, max_rounds=400, seed=45,
+                                            trace_spread=True), 256),
+    "faulty_d32_dlpsw_split_sa2048": (Config(n_nodes=40000, topology="regular", degree=32, rule="dlpsw", trim=5,
+                                             fault_model="byzantine", n_faulty=1000, byz_strategy="split",
+                                             byz_delta=0.1, loss_p=0.05, eps=1e-9, max_rounds=300, seed=46,
+                                             trace_spread=True), 2048),
+    "faulty_wmsr_d16_t5_crash_sa1024": (Config(n_nodes=30000, topology="regular", degree=16, rule="wmsr", trim=5,
+                                               fault_model="crash", n_faulty=600, crash_window=4, loss_p=0.1,
+                                               eps=1e-8, max_rounds=300, seed=47, trace_spread=True), 1024),
+    "faulty_cfg4_byz_shape_2e17": (preset("cfg4_byz", n_nodes=1 << 17, trace_spread=True), 16384),
 }
 
 
@@ -70,8 +96,10 @@ def test_binned_matches_oracle_and_per_lane(oracle_mod, name):
     with env(ACSIM_BIN_SA=sa):
         kb, rb, xb, tb = run_gpu(cfg)
     assert kb.startswith("k_bin_scatter"), kb
-    if name.startswith("two_level"):
+    if "two_level" in name:
         assert "k_bin_regroup" in kb, kb
+    if name.startswith("faulty"):
+        assert ",faulty>" in kb, kb
     with env(ACSIM_BINNED=0):
         kr, rr, xr, tr = run_gpu(cfg)
     assert kr.startswith("k_round_regular"), kr
@@ -143,3 +171,41 @@ def test_two_level_virtual_partitions(oracle_mod, parts):
         o.run()
         assert np.array_equal(o.rounds(), pr)
         assert np.array_equal(bits(o.values(0)), px)
+
+
+def test_faulty_full_cfg4_byz_matches_per_lane():
+    """Full-size cfg4_byz (N = 2^20, 1048 Byzantine RANDOM senders): binned vs per-lane bit for bit."""
+    cfg = preset("cfg4_byz", max_rounds=25, trace_spread=True)
+    kb, rb, xb, tb = run_gpu(cfg)
+    assert kb.startswith("k_bin_scatter") and kb.endswith("+k_bin_tag"), kb
+    with env(ACSIM_BINNED=0):
+        _, rr, xr, tr = run_gpu(cfg)
+    assert np.array_equal(rb, rr) and np.array_equal(xb, xr) and np.array_equal(tb, tr)
+
+
+def test_faulty_chunks_resume_and_partitions(oracle_mod):
+    """Crash + loss: stepped rounds, set_state resume and 3 virtual partitions against one run."""
+    cfg = Config(n_nodes=45000, topology="regular", degree=16, rule="trimmed", trim=5, fault_model="crash",
+                 n_faulty=900, crash_window=8, loss_p=0.1, eps=1e-9, max_rounds=200, seed=48, trace_spread=True)
+    with env(ACSIM_BIN_SA=512):
+        with acsim.Simulator(cfg, device=0) as g:
+            assert ",faulty>" in g.kernel_name()
+            g.run()
+            ref, rounds = bits(g.values(0)), int(g.rounds()[0])
+        with acsim.Simulator(cfg, device=0) as g:
+            g.round(3)
+            mid = g.values(0).copy()
+            g.round(4)
+            g.run()
+            assert int(g.rounds()[0]) == rounds and np.array_equal(bits(g.values(0)), ref)
+        with acsim.Simulator(cfg, device=0) as g:
+            g.set_state(3, mid[None, :])
+            g.run()
+            assert np.array_equal(bits(g.values(0)), ref)
+        with acsim.Simulator(cfg, partitions=3) as p:
+            assert ",faulty>" in p.kernel_name(), p.kernel_name()
+            p.run()
+            assert int(p.rounds()[0]) == rounds and np.array_equal(bits(p.values(0)), ref)
+    with oracle_mod.OracleSimulator(cfg, threads=8) as o:
+        o.run()
+        assert int(o.rounds()[0]) == rounds and np.array_equal(bits(o.values(0)), ref)
