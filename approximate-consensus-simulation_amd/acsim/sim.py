@@ -181,8 +181,9 @@ class Simulator:
         return out.reshape(self.N, d)
 
     # -------------------------------------------------------------------------- measurement
-    def set_kernel_timing(self, enable: bool) -> None:
-        self._chk(self._lib.acs_set_kernel_timing(self._h, 1 if enable else 0))
+    def set_kernel_timing(self, enable, every: int = 1) -> None:
+        """Bracket round-kernel launches with HIP events (every `every`-th round when enabled)."""
+        self._chk(self._lib.acs_set_kernel_timing(self._h, max(1, int(every)) if enable else 0))
 
     def kernel_timing(self):
         """(total_ms, launches, kernel_name) of the round kernel since timing was enabled."""

@@ -95,7 +95,8 @@ struct acs_sim {
     uint32_t* dcounts = nullptr;   // dense path: |B|, #Byzantine, #crash-silent
     std::vector<Part> parts;       // virtual partitions 1..P-1 (partition 0 uses x / ell)
     // kernel timing (bench)
-    bool timing = false;
+    uint32_t timing = 0;           // 0 off, else bracket every timing-th round (sampling)
+    uint64_t timing_ctr = 0;
     std::vector<hipEvent_t> ev;    // pairs (start, stop)
     size_t ev_used = 0;
     double timed_ms = 0.0;
@@ -286,7 +287,7 @@ static int harvest_timing(acs_sim* s) {
 
 static int timing_begin(acs_sim* s, hipEvent_t* e1) {
     *e1 = nullptr;
-    if (!s->timing) return ACS_OK;
+    if (!s->timing || s->timing_ctr++ % s->timing != 0) return ACS_OK;
     if (s->ev_used + 2 > 4096) {
         int rc = harvest_timing(s);
         if (rc) return rc;
@@ -984,7 +985,8 @@ int acs_set_kernel_timing(acs_sim* s, int enable) {
     HIP_TRY(hipSetDevice(s->device));
     int rc = harvest_timing(s);
     if (rc) return rc;
-    s->timing = enable != 0;
+    s->timing = enable > 0 ? (uint32_t)enable : 0u;
+    s->timing_ctr = 0;
     s->timed_ms = 0.0;
     s->timed_launches = 0;
     return ACS_OK;

@@ -12,7 +12,9 @@ The roofline object prices the dominant kernel at SURVEY §8(d)'s algorithmic 40
 launch processes, divided by its average device duration measured with HIP events on the
 handle's stream over the timed region.  On cfg4 the round is the binned exchange
 (csrc/round_binned.hip): two launches, k_bin_scatter then k_bin_gather, bracketed together by
-one event pair per round, so "one launch" here means that pair (the ε finalize is excluded).
+one event pair, so "one launch" here means that pair (the ε finalize is excluded).  Every
+--event-every-th timed round (default 10) is bracketed: an event pair idles the stream for
+~5 µs, which would otherwise inflate ms_per_step by ~7 %.
 `traffic` is the pair's measured HBM bytes per round (profiles/pmc_cfg4.json, FETCH_SIZE x 2 +
 WRITE_SIZE, tools/traffic_json.py).  cpu_baseline times the CPU oracle (this
 repo's spec restatement, oracle/) on rank 0 on a bounded sample of the same workload.
@@ -45,6 +47,9 @@ def parse():
                    help="target CPU work for the bounded cpu_baseline sample")
     p.add_argument("--no-event-timing", action="store_true",
                    help="skip per-launch HIP events (roofline then uses ms_per_step)")
+    p.add_argument("--event-every", type=int, default=10,
+                   help="bracket every k-th timed round with HIP events (each pair idles the "
+                        "stream ~5 us, so sampling keeps the timed region representative)")
     return p.parse_args()
 
 
@@ -108,7 +113,7 @@ def main():
 
     if a.warmup:
         sim.round(a.warmup)
-    sim.set_kernel_timing(not a.no_event_timing)
+    sim.set_kernel_timing(not a.no_event_timing, every=a.event_every)
     barrier_sync()
     t0 = time.perf_counter()
     sim.round(a.steps)

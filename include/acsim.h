@@ -199,9 +199,11 @@ int acs_get_fault_status(struct acs_sim* sim, uint32_t* out, uint64_t n);
 /* Adjacency (§A.3) of a RANDOM_REGULAR graph: out[i*d + t] = nbr(i, t). */
 int acs_get_neighbors(struct acs_sim* sim, uint32_t* out, uint64_t n);
 
-/* Kernel timing (bench measurement, §8d): while enabled, HIP events bracket every launch of
- * the round kernel on the handle's stream; acs_get_kernel_timing returns the summed device time
- * and launch count since the last reset, plus the name of the round kernel in use. */
+/* Kernel timing (bench measurement, §8d): while enabled, HIP events bracket the launches of the
+ * round kernel on the handle's stream — every round for enable == 1, every enable-th round for
+ * enable > 1 (each event pair idles the stream for a few µs, so the bench samples); 0 disables.
+ * acs_get_kernel_timing returns the summed device time and bracketed launch count since the
+ * last reset, plus the name of the round kernel in use. */
 int acs_set_kernel_timing(struct acs_sim* sim, int enable);
 int acs_get_kernel_timing(struct acs_sim* sim, double* total_ms, uint64_t* launches,
                           char* kernel_name, uint64_t name_cap);

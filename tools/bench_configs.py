@@ -31,7 +31,7 @@ def run(name, **kw):
     t0 = time.perf_counter()
     sim = acsim.Simulator(cfg)
     t_setup = time.perf_counter() - t0
-    sim.set_kernel_timing(True)
+    sim.set_kernel_timing(True, every=10)
     t0 = time.perf_counter()
     res = sim.run()
     wall = time.perf_counter() - t0
