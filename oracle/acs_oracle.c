@@ -119,10 +119,19 @@ uint32_t acso_drop_threshold(double p) {
     return (uint32_t)t;
 }
 
+/* ---------------------------------------------------------------- §A.0 value type */
+
+/* DESIGN.md §9 fp32 mode (ACS_F32): values are binary32 and every arithmetic step rounds to
+ * binary32.  The oracle keeps them in doubles and rounds each +, -, *, / result with rnd():
+ * for these operations on binary32 operands, the double result rounded to binary32 equals the
+ * binary32 result (53 >= 2*24 + 2), so this is exact binary32 arithmetic.  Comparisons, min
+ * and max need no rounding. */
+static double rnd(int f32, double v) { return f32 ? (double)(float)v : v; }
+
 /* ---------------------------------------------------------------- §A.7 rules */
 
 /* §A.7 tree_sum: pad to the next power of two with +0.0, then stride-halving pairwise adds. */
-double acso_tree_sum(const double* a, uint64_t n) {
+static double tree_sum_t(const double* a, uint64_t n, int f32) {
     if (n == 0) return 0.0;
     uint64_t P = 1;
     while (P < n) P <<= 1;
@@ -130,11 +139,13 @@ double acso_tree_sum(const double* a, uint64_t n) {
     double* w = P <= 128 ? stackbuf : (double*)malloc(P * sizeof(double));
     for (uint64_t k = 0; k < P; ++k) w[k] = k < n ? a[k] : 0.0;
     for (uint64_t s = P / 2; s >= 1; s /= 2)
-        for (uint64_t k = 0; k < s; ++k) w[k] = w[k] + w[k + s];
+        for (uint64_t k = 0; k < s; ++k) w[k] = rnd(f32, w[k] + w[k + s]);
     double r = w[0];
     if (w != stackbuf) free(w);
     return r;
 }
+
+double acso_tree_sum(const double* a, uint64_t n) { return tree_sum_t(a, n, 0); }
 
 static int cmp_double(const void* a, const void* b) {
     double x = *(const double*)a, y = *(const double*)b;
@@ -156,8 +167,8 @@ static void sort_asc(double* a, uint64_t m) {
 
 /* §A.7: apply the rule to the m entries of S (S is reordered in place); xi is the receiver's own
  * value (W-MSR only). */
-static double apply_rule(uint32_t rule, uint32_t t, double* S, uint64_t m, double* scratch, double xi) {
-    if (rule == ACS_RULE_AVERAGE) return acso_tree_sum(S, m) / (double)m;
+static double apply_rule(uint32_t rule, uint32_t t, double* S, uint64_t m, double* scratch, double xi, int f32) {
+    if (rule == ACS_RULE_AVERAGE) return rnd(f32, tree_sum_t(S, m, f32) / (double)m);
     sort_asc(S, m);
     if (rule == ACS_RULE_WMSR) {
         /* drop min(t, #below) smallest and min(t, #above) largest entries, where
@@ -168,16 +179,16 @@ static double apply_rule(uint32_t rule, uint32_t t, double* S, uint64_t m, doubl
             else if (S[k] > xi) ++ng;
         }
         const uint64_t lo = nl < t ? nl : t, hi = ng < t ? ng : t, nw = m - lo - hi;
-        return acso_tree_sum(S + lo, nw) / (double)nw;
+        return rnd(f32, tree_sum_t(S + lo, nw, f32) / (double)nw);
     }
     const double* R = S + t;
     const uint64_t nr = m - 2ull * t;
-    if (rule == ACS_RULE_TRIMMED_MEAN) return acso_tree_sum(R, nr) / (double)nr;
-    if (rule == ACS_RULE_MIDPOINT) return (R[0] + R[nr - 1]) * 0.5;
+    if (rule == ACS_RULE_TRIMMED_MEAN) return rnd(f32, tree_sum_t(R, nr, f32) / (double)nr);
+    if (rule == ACS_RULE_MIDPOINT) return rnd(f32, rnd(f32, R[0] + R[nr - 1]) * 0.5);
     /* DLPSW_SELECT: Q = R[0], R[t], R[2t], ... */
     uint64_t nq = 0;
     for (uint64_t k = 0; k < nr; k += t) scratch[nq++] = R[k];
-    return acso_tree_sum(scratch, nq) / (double)nq;
+    return rnd(f32, tree_sum_t(scratch, nq, f32) / (double)nq);
 }
 
 /* ---------------------------------------------------------------- validation (§A.8 constraints) */
@@ -246,7 +257,10 @@ int acso_validate(const acs_config* c) {
     if (c->mask_group < 1) return fail(ACS_EINVAL, "mask_group must be >= 1");
     if (!(c->eps >= 0.0 && c->eps <= 1e300)) return fail(ACS_EINVAL, "eps must be finite, >= 0");
     if (c->termination > ACS_TERM_FIXED) return fail(ACS_EINVAL, "unknown termination");
-    if (c->dtype != ACS_F64) return fail(ACS_EUNSUPPORTED, "only ACS_F64 is implemented");
+    if (c->dtype != ACS_F64 && c->dtype != ACS_F32) return fail(ACS_EINVAL, "unknown dtype %u", c->dtype);
+    if (c->dtype == ACS_F32 && c->fault_model == ACS_FAULT_BYZANTINE &&
+        !(fabs(c->byz_delta) <= 1e30 && fabs(c->byz_const) <= 1e30))
+        return fail(ACS_EINVAL, "fp32: byz_delta / byz_const must satisfy |.| <= 1e30");
     if (c->delay_max > 64) return fail(ACS_EINVAL, "delay_max must be <= 64");
     if (c->reserved0 != 0) return fail(ACS_EINVAL, "reserved0 must be 0");
     if (c->trace_spread && c->n_instances * ((uint64_t)c->max_rounds + 1) > (1ull << 28))
@@ -274,6 +288,7 @@ struct acso_sim {
     double* hi;              /* B */
     double* trace;           /* B*(max_rounds+1) or NULL */
     int threads;
+    int f32;                 /* ACS_F32: binary32 values, held exactly in the double arrays */
 };
 
 static int cmp_u64(const void* a, const void* b) {
@@ -297,7 +312,7 @@ static void honest_minmax(const acso_sim* s, uint64_t b) {
 
 static void after_update(acso_sim* s, uint64_t b) {
     honest_minmax(s, b);
-    const double spread = s->hi[b] - s->lo[b];
+    const double spread = rnd(s->f32, s->hi[b] - s->lo[b]);
     const uint32_t r = s->rounds[b];
     if (s->trace) s->trace[b * ((uint64_t)s->c.max_rounds + 1) + r] = spread;
     s->converged[b] = spread <= s->c.eps;
@@ -317,6 +332,7 @@ int acso_create(const acs_config* cfg, acso_sim** out) {
     s->m = cfg->topology == ACS_TOPO_COMPLETE ? s->N : (uint64_t)cfg->degree + 1;
     s->thr = acso_drop_threshold(cfg->loss_p);
     s->threads = cfg->omp_threads ? (int)cfg->omp_threads : 1;
+    s->f32 = cfg->dtype == ACS_F32;
     const uint64_t gseed = cfg->graph_seed ? cfg->graph_seed : cfg->seed;
     const uint64_t BN = s->B * s->N;
     s->status = (uint32_t*)malloc(BN * sizeof(uint32_t));
@@ -354,10 +370,11 @@ int acso_create(const acs_config* cfg, acso_sim** out) {
         const uint32_t b = (uint32_t)(cfg->instance_offset + lb);
         uint32_t* st = s->status + lb * s->N;
         double* x = s->x + lb * s->N;
-        /* §A.2 initial values */
+        /* §A.2 initial values (fp32: (draw(INIT,b,0,2i) >> 8) * 2^-24, exact in binary32) */
         for (uint64_t i = 0; i < s->N; ++i)
-            x[i] = acso_u53(acso_draw(cfg->seed, ACS_STREAM_INIT, b, 0, 2 * i),
-                            acso_draw(cfg->seed, ACS_STREAM_INIT, b, 0, 2 * i + 1));
+            x[i] = s->f32 ? (double)(acso_draw(cfg->seed, ACS_STREAM_INIT, b, 0, 2 * i) >> 8) * 0x1p-24
+                          : acso_u53(acso_draw(cfg->seed, ACS_STREAM_INIT, b, 0, 2 * i),
+                                     acso_draw(cfg->seed, ACS_STREAM_INIT, b, 0, 2 * i + 1));
         /* §A.4 fault set: the f smallest (draw(FAULTSET,b,0,i), i) pairs */
         for (uint64_t i = 0; i < s->N; ++i) st[i] = HONEST;
         if (cfg->fault_model != ACS_FAULT_NONE && cfg->n_faulty > 0) {
@@ -440,12 +457,22 @@ void acso_destroy(acso_sim* s) {
     free(s);
 }
 
-/* §A.4 Byzantine value on slot s to receiver i in round r. */
+/* §A.4 Byzantine value on slot s to receiver i in round r.  fp32: Δ and c are
+ * rounded to binary32 once, RANDOM uses u24 = (draw(BYZ,b,r,2s) >> 8) * 2^-24, and every step
+ * rounds to binary32 in the order written below. */
 static double byz_value(const acso_sim* s, uint32_t b, uint32_t r, uint64_t i, uint64_t slot,
                         double lo, double hi) {
     const acs_config* c = &s->c;
+    if (s->f32) {
+        const double dl = (double)(float)c->byz_delta;
+        if (c->byz_strategy == ACS_BYZ_SPLIT) return (i & 1u) == 0 ? rnd(1, hi + dl) : rnd(1, lo - dl);
+        if (c->byz_strategy == ACS_BYZ_CONSTANT) return (double)(float)c->byz_const + 0.0;
+        const double u = (double)(acso_draw(c->seed, ACS_STREAM_BYZ, b, r, 2 * slot) >> 8) * 0x1p-24;
+        const double width = rnd(1, rnd(1, hi - lo) + 2.0 * dl);
+        return rnd(1, rnd(1, lo - dl) + rnd(1, u * width));
+    }
     if (c->byz_strategy == ACS_BYZ_SPLIT) return (i & 1u) == 0 ? hi + c->byz_delta : lo - c->byz_delta;
-    if (c->byz_strategy == ACS_BYZ_CONSTANT) return c->byz_const;
+    if (c->byz_strategy == ACS_BYZ_CONSTANT) return c->byz_const + 0.0;   /* canonical +0.0 */
     const double u = acso_u53(acso_draw(c->seed, ACS_STREAM_BYZ, b, r, 2 * slot),
                               acso_draw(c->seed, ACS_STREAM_BYZ, b, r, 2 * slot + 1));
     const double width = (hi - lo) + 2.0 * c->byz_delta;
@@ -508,7 +535,7 @@ static void step_instance(acso_sim* s, uint64_t lb) {
                 S[0] = x[i];
                 for (uint64_t t = 0; t < deg; ++t)
                     S[1 + t] = resolve(s, b, bG, r, x, st, i, s->colidx[rp + t], rp + t, lo, hi);
-                xn[i] = apply_rule(c->rule, c->trim, S, deg + 1, scratch, x[i]);
+                xn[i] = apply_rule(c->rule, c->trim, S, deg + 1, scratch, x[i], s->f32);
                 continue;
             } else {
                 const uint64_t d = c->degree;
@@ -516,7 +543,7 @@ static void step_instance(acso_sim* s, uint64_t lb) {
                 for (uint64_t t = 0; t < d; ++t)
                     S[1 + t] = resolve(s, b, bG, r, x, st, i, s->nbr[i * d + t], i * d + t, lo, hi);
             }
-            xn[i] = apply_rule(c->rule, c->trim, S, m, scratch, x[i]);
+            xn[i] = apply_rule(c->rule, c->trim, S, m, scratch, x[i], s->f32);
         }
         free(S);
     }
@@ -536,7 +563,7 @@ static void fill_info(const acso_sim* s, acs_round_info* out) {
     uint32_t rmax = 0;
     for (uint64_t b = 0; b < s->B; ++b) {
         nd += s->done[b];
-        const double v = s->hi[b] - s->lo[b];
+        const double v = rnd(s->f32, s->hi[b] - s->lo[b]);
         if (v > sp) sp = v;
         if (s->rounds[b] > rmax) rmax = s->rounds[b];
     }
@@ -571,7 +598,7 @@ int acso_run(acso_sim* s, acs_result* out) {
             if (s->rounds[b] > out->rounds_max) out->rounds_max = s->rounds[b];
             out->n_converged += s->converged[b];
             out->node_rounds += s->N * (uint64_t)s->rounds[b];
-            const double v = s->hi[b] - s->lo[b];
+            const double v = rnd(s->f32, s->hi[b] - s->lo[b]);
             if (v > out->final_spread_max) out->final_spread_max = v;
         }
         out->wall_seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
@@ -599,7 +626,7 @@ int acso_get_instance_converged(acso_sim* s, uint8_t* out, uint64_t n) {
 
 int acso_get_instance_spread(acso_sim* s, double* out, uint64_t n) {
     if (!s || !out || n < s->B) return fail(ACS_EINVAL, "bad args");
-    for (uint64_t b = 0; b < s->B; ++b) out[b] = s->hi[b] - s->lo[b];
+    for (uint64_t b = 0; b < s->B; ++b) out[b] = rnd(s->f32, s->hi[b] - s->lo[b]);
     return ACS_OK;
 }
 
@@ -616,6 +643,9 @@ int acso_get_spread_trace(acso_sim* s, uint64_t b, double* out, uint64_t n, uint
 int acso_set_state(acso_sim* s, uint32_t round, const double* x, uint64_t n) {
     if (!s || !x || n != s->B * s->N) return fail(ACS_EINVAL, "set_state needs B*N values");
     if (round > s->c.max_rounds) return fail(ACS_EINVAL, "round > max_rounds");
+    if (s->f32)
+        for (uint64_t k = 0; k < n; ++k)
+            if ((double)(float)x[k] != x[k]) return fail(ACS_EINVAL, "fp32 set_state: values must be binary32");
     memcpy(s->x, x, n * sizeof(double));
     /* bounded-delay history restarts from x: every past slot holds x^round */
     if (s->hist)

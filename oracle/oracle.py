@@ -163,11 +163,16 @@ class OracleSimulator:
         _chk(self._lib.acso_run(self._h, C.byref(res)))
         return res
 
+    @property
+    def f32(self):
+        return int(self._c.dtype) == _abi.F32
+
     def values(self, instance=0):
+        """Node values in the config dtype (fp32 values are held exactly as doubles in C)."""
         out = np.empty(self.N, dtype=np.float64)
         _chk(self._lib.acso_get_values(self._h, int(instance),
                                        out.ctypes.data_as(C.POINTER(C.c_double)), out.size))
-        return out
+        return out.astype(np.float32) if self.f32 else out
 
     def all_values(self):
         return np.stack([self.values(b) for b in range(self.B)])

@@ -2,7 +2,8 @@
 
 Written separately from oracle/acs_oracle.c (vectorised over receivers, numpy's own sort, no
 shared code) so that agreement between the two pins the C oracle.  Each function cites the §A
-rule it follows.  numpy performs every fp64 operation as a single IEEE-rounded op (no FMA).
+rule it follows.  numpy performs every fp64 / fp32 operation as a single IEEE-rounded op (no
+FMA); fp32 mode runs the same code on float32 arrays and float32 constants.
 """
 from __future__ import annotations
 
@@ -95,12 +96,12 @@ def drop_threshold(p: float) -> int:
 
 def tree_sum_rows(a: np.ndarray) -> np.ndarray:
     """§A.7 tree_sum of every row: pad with +0.0 to a power of two, stride-halving adds."""
-    a = np.asarray(a, dtype=np.float64)
+    a = np.asarray(a)
     n = a.shape[-1]
     P = 1
     while P < n:
         P *= 2
-    w = np.zeros(a.shape[:-1] + (P,), dtype=np.float64)
+    w = np.zeros(a.shape[:-1] + (P,), dtype=a.dtype)
     w[..., :n] = a
     s = P // 2
     while s >= 1:
@@ -112,27 +113,28 @@ def tree_sum_rows(a: np.ndarray) -> np.ndarray:
 def apply_rule(rule: int, t: int, S: np.ndarray, xi=None) -> np.ndarray:
     """§A.7 on rows of S (entry order preserved for AVERAGE); xi = receivers' own values (W-MSR)."""
     m = S.shape[1]
+    ft = S.dtype.type
     if rule == 0:
-        return tree_sum_rows(S) / float(m)
+        return tree_sum_rows(S) / ft(m)
     if rule == 4:
         # W-MSR (DESIGN.md §9): drop min(t, #below x_i) smallest and min(t, #above x_i) largest;
         # zero padding past the window leaves the stride-halving sum unchanged (no -0.0 values)
         Ss = np.sort(S, axis=1)
-        xi = np.asarray(xi, dtype=np.float64)[:, None]
+        xi = np.asarray(xi, dtype=S.dtype)[:, None]
         lo = np.minimum(t, (Ss < xi).sum(axis=1))
         hi = np.minimum(t, (Ss > xi).sum(axis=1))
         nw = m - lo - hi
         k = np.arange(m)[None, :]
         idx = np.minimum(lo[:, None] + k, m - 1)
-        W = np.where(k < nw[:, None], np.take_along_axis(Ss, idx, axis=1), 0.0)
-        return tree_sum_rows(W) / nw.astype(np.float64)
+        W = np.where(k < nw[:, None], np.take_along_axis(Ss, idx, axis=1), ft(0))
+        return tree_sum_rows(W) / nw.astype(S.dtype)
     R = np.sort(S, axis=1)[:, t:m - t]
     if rule == 1:
-        return tree_sum_rows(R) / float(R.shape[1])
+        return tree_sum_rows(R) / ft(R.shape[1])
     if rule == 2:
-        return (R[:, 0] + R[:, -1]) * 0.5
+        return (R[:, 0] + R[:, -1]) * ft(0.5)
     Q = R[:, ::t]
-    return tree_sum_rows(Q) / float(Q.shape[1])
+    return tree_sum_rows(Q) / ft(Q.shape[1])
 
 
 class NpSim:
@@ -163,13 +165,18 @@ class NpSim:
             for t in range(self.d):
                 cols.append(feistel(N, gseed, t >> 1, i, inverse=bool(t & 1)))
             self.nbr = np.stack(cols, axis=1).astype(np.int64)
-        self.x = np.empty((self.B, N))
+        self.f32 = _enum("dtype", getattr(cfg, "dtype", "f64")) == 1
+        self.ft = np.float32 if self.f32 else np.float64
+        self.x = np.empty((self.B, N), dtype=self.ft)
         self.status = np.full((self.B, N), HONEST, dtype=np.uint64)
         self.gb = [int(cfg.instance_offset) + lb for lb in range(self.B)]
         idx = np.arange(N, dtype=np.uint64)
         for lb, b in enumerate(self.gb):
             w = draw(self.seed, INIT, b, 0, 2 * idx), draw(self.seed, INIT, b, 0, 2 * idx + 1)
-            self.x[lb] = u53(*w)
+            if self.f32:   # (draw(INIT,b,0,2i) >> 8) * 2^-24
+                self.x[lb] = (w[0] >> np.uint32(8)).astype(np.float32) * np.float32(2.0 ** -24)
+            else:
+                self.x[lb] = u53(*w)
             f = int(cfg.n_faulty)
             if self.fault and f:
                 keys = (draw(self.seed, FAULTSET, b, 0, idx).astype(np.uint64) << np.uint64(32)) | idx
@@ -184,8 +191,8 @@ class NpSim:
         self.D = int(getattr(cfg, "delay_max", 0))
         self.hist = [[self.x[lb].copy()] for lb in range(self.B)]
         self.trace = [[] for _ in range(self.B)]
-        self.lo = np.zeros(self.B)
-        self.hi = np.zeros(self.B)
+        self.lo = np.zeros(self.B, dtype=self.ft)
+        self.hi = np.zeros(self.B, dtype=self.ft)
         self.done = np.zeros(self.B, dtype=bool)
         self.converged = np.zeros(self.B, dtype=bool)
         for lb in range(self.B):
@@ -195,7 +202,7 @@ class NpSim:
         h = self.status[lb] == HONEST
         xs = self.x[lb][h]
         self.lo[lb], self.hi[lb] = xs.min(), xs.max()
-        sp = self.hi[lb] - self.lo[lb]
+        sp = float(self.hi[lb] - self.lo[lb])
         self.trace[lb].append(sp)
         self.converged[lb] = sp <= self.cfg.eps
         self.done[lb] = (self.term == 0 and sp <= self.cfg.eps) or self.rounds[lb] >= self.cfg.max_rounds
@@ -269,16 +276,21 @@ class NpSim:
                         V[mk] = self.hist[lb][r - dv][J[mk]]
             byzm = (sj == BYZ) & ~selfm & ~missing
             if byzm.any():
-                d = float(cfg.byz_delta)
+                ft = self.ft
+                d = ft(cfg.byz_delta)
+                lo, hi = ft(lo), ft(hi)
                 if self.byz == 0:
                     rowv = np.where((A % 2) == 0, hi + d, lo - d)
                     V[byzm] = np.broadcast_to(rowv[:, None], V.shape)[byzm]
                 elif self.byz == 2:
-                    V[byzm] = float(cfg.byz_const)
+                    V[byzm] = ft(cfg.byz_const) + ft(0)
                 else:
                     s2 = slots[byzm] * np.uint64(2)
-                    u = u53(draw(self.seed, BYZS, b, r, s2), draw(self.seed, BYZS, b, r, s2 + np.uint64(1)))
-                    V[byzm] = (lo - d) + u * ((hi - lo) + 2.0 * d)
+                    if self.f32:   # u24 = (draw(BYZ,b,r,2s) >> 8) * 2^-24
+                        u = (draw(self.seed, BYZS, b, r, s2) >> np.uint32(8)).astype(np.float32) * np.float32(2.0 ** -24)
+                    else:
+                        u = u53(draw(self.seed, BYZS, b, r, s2), draw(self.seed, BYZS, b, r, s2 + np.uint64(1)))
+                    V[byzm] = (lo - d) + u * ((hi - lo) + ft(2) * d)
             V[missing | selfm] = np.broadcast_to(x[A][:, None], V.shape)[missing | selfm]
         return V
 

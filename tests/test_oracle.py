@@ -173,3 +173,58 @@ def test_oracle_resume_exact(oracle_mod):
         b.run()
         assert b.rounds().tolist() == ra
         assert b.values(0).tobytes() == final
+
+
+# fp32 mode: binary32 values and arithmetic; the C oracle rounds every step of its
+# double arithmetic to binary32, numpy runs float32 arrays — they must agree bit for bit.
+F32_CFGS = [
+    Config(n_nodes=50, topology="complete", rule="midpoint", trim=4, fault_model="crash", n_faulty=6,
+           crash_window=3, loss_p=0.15, eps=1e-6, max_rounds=200, seed=21, trace_spread=True, dtype="f32"),
+    Config(n_nodes=300, topology="regular", degree=12, rule="dlpsw", trim=3, fault_model="byzantine",
+           n_faulty=20, byz_strategy="split", byz_delta=0.5, eps=1e-6, max_rounds=300, seed=9,
+           trace_spread=True, dtype="f32"),
+    Config(n_nodes=10, n_instances=7, topology="complete", rule="average", loss_p=0.4, mask_group=3,
+           eps=0.0, max_rounds=25, termination="fixed", seed=2, trace_spread=True, dtype="f32"),
+    Config(n_nodes=400, topology="regular", degree=16, rule="wmsr", trim=4, fault_model="byzantine",
+           n_faulty=30, byz_strategy="random", byz_delta=0.3, loss_p=0.1, eps=1e-6, max_rounds=300,
+           seed=13, trace_spread=True, dtype="f32"),
+    Config(n_nodes=2000, topology="regular", degree=32, rule="trimmed", trim=5, eps=1e-6,
+           max_rounds=300, seed=0, trace_spread=True, dtype="f32"),
+    Config(n_nodes=300, topology="regular", degree=8, rule="trimmed", trim=2, fault_model="byzantine",
+           n_faulty=10, byz_strategy="constant", byz_const=0.7, loss_p=0.05, delay_max=3, eps=1e-6,
+           max_rounds=300, seed=16, trace_spread=True, dtype="f32"),
+]
+
+
+@pytest.mark.parametrize("cfg", F32_CFGS, ids=["complete_mid_crash_drop", "regular_dlpsw_split",
+                                              "batched_avg_fixed_grouped", "regular_wmsr_byzrandom_drop",
+                                              "cfg4_shaped", "regular_delay3_const_drop"])
+def test_oracle_matches_numpy_f32(oracle_mod, cfg):
+    with oracle_mod.OracleSimulator(cfg) as o:
+        o.run()
+        n = S.NpSim(cfg)
+        n.run()
+        assert n.x.dtype == np.float32
+        xo = o.all_values()
+        assert xo.dtype == np.float32
+        assert np.array_equal(o.rounds(), n.rounds)
+        assert np.array_equal(xo.view(np.uint32), n.x.view(np.uint32))
+        for b in range(cfg.n_instances):
+            assert np.array_equal(o.spread_trace(b).view(np.uint64), np.array(n.trace[b]).view(np.uint64))
+        assert int(o.rounds().max()) > 2
+
+
+def test_oracle_f32_init_and_resume(oracle_mod):
+    cfg = preset("cfg4_eps", n_nodes=3000, loss_p=0.1, dtype="f32", eps=1e-6)
+    with oracle_mod.OracleSimulator(cfg) as a:
+        x0 = a.values(0)
+        w = np.array([oracle_mod.draw(0, 0, 0, 0, 2 * i) for i in range(8)], dtype=np.uint64)
+        assert np.array_equal(x0[:8], ((w >> 8).astype(np.float64) * 2.0 ** -24).astype(np.float32))
+        a.round(4)
+        x4 = a.values(0)
+        a.run()
+        final, ra = a.values(0).tobytes(), a.rounds().tolist()
+    with oracle_mod.OracleSimulator(cfg) as b:
+        b.set_state(4, x4)
+        b.run()
+        assert b.rounds().tolist() == ra and b.values(0).tobytes() == final
