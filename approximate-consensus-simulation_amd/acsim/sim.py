@@ -123,14 +123,19 @@ class Simulator:
         self._chk(self._lib.acs_sync(self._h))
 
     # -------------------------------------------------------------------------- state access
+    @property
+    def value_dtype(self):
+        """numpy dtype of node values: float64, or float32 for dtype="f32" (DESIGN.md §9)."""
+        return np.float32 if int(self._c.dtype) == _abi.F32 else np.float64
+
     def values(self, instance: int = 0) -> np.ndarray:
-        out = np.empty(self.N, dtype=np.float64)
+        out = np.empty(self.N, dtype=self.value_dtype)
         self._chk(self._lib.acs_get_values(self._h, int(instance), out.ctypes.data, out.size))
         return out
 
     def partition_values(self, partition: int) -> np.ndarray:
         """Virtual partitions: the private x copy of one partition."""
-        out = np.empty(self.N, dtype=np.float64)
+        out = np.empty(self.N, dtype=self.value_dtype)
         self._chk(self._lib.acs_get_partition_values(self._h, int(partition), out.ctypes.data, out.size))
         return out
 
@@ -164,7 +169,11 @@ class Simulator:
         return out[: got.value].copy()
 
     def set_state(self, round: int, x: np.ndarray) -> None:
-        x = np.ascontiguousarray(x, dtype=np.float64).reshape(-1)
+        xv = np.asarray(x)
+        if self.value_dtype == np.float32 and xv.dtype != np.float32 and not np.array_equal(
+                xv.astype(np.float32).astype(xv.dtype), xv):
+            raise ValueError("fp32 set_state: values must be exactly representable in binary32")
+        x = np.ascontiguousarray(xv, dtype=self.value_dtype).reshape(-1)
         self._chk(self._lib.acs_set_state(self._h, int(round), x.ctypes.data, x.size))
 
     def fault_status(self) -> np.ndarray:

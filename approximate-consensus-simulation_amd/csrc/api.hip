@@ -71,6 +71,8 @@ struct acs_sim {
     double* x[2] = {nullptr, nullptr};   // x[k] = xb(k): the synchronous double buffer
     double* xall = nullptr;        // H value buffers of B*Npad (+2) doubles, x^q in buffer q % H
     uint64_t xstride = 0;          // elements per buffer
+    uint32_t es = 8;               // value bytes: 8 (ACS_F64) or 4 (ACS_F32)
+    bool f32 = false;
     uint32_t H = 2;                // delay_max + 2: x^{r-D} .. x^r read, x^{r+1} written
     uint32_t* ell = nullptr;       // rows [row0, row0 + rows_per) of this rank
     uint32_t* status = nullptr;
@@ -170,7 +172,10 @@ static int validate(const acs_config* c) {
     if (c->mask_group < 1) return fail(ACS_EINVAL, "mask_group must be >= 1");
     if (!(c->eps >= 0.0 && c->eps <= 1e300)) return fail(ACS_EINVAL, "eps must be finite, >= 0");
     if (c->termination > ACS_TERM_FIXED) return fail(ACS_EINVAL, "unknown termination");
-    if (c->dtype != ACS_F64) return fail(ACS_EUNSUPPORTED, "only ACS_F64 is implemented");
+    if (c->dtype != ACS_F64 && c->dtype != ACS_F32) return fail(ACS_EINVAL, "unknown dtype %u", c->dtype);
+    if (c->dtype == ACS_F32 && c->fault_model == ACS_FAULT_BYZANTINE &&
+        !(fabs(c->byz_delta) <= 1e30 && fabs(c->byz_const) <= 1e30))
+        return fail(ACS_EINVAL, "fp32: byz_delta / byz_const must satisfy |.| <= 1e30");
     if (c->delay_max > 64) return fail(ACS_EINVAL, "delay_max must be <= 64");
     if (c->reserved0 != 0) return fail(ACS_EINVAL, "reserved0 must be 0");
     if (c->trace_spread && c->n_instances * ((uint64_t)c->max_rounds + 1) > (1ull << 28))
@@ -223,7 +228,14 @@ static void release(acs_sim* s) {
 }
 
 // value buffer holding x^q
-static double* xb(const acs_sim* s, uint32_t q) { return s->xall + (uint64_t)(q % s->H) * s->xstride; }
+// value buffer q % H (typed double* for the kernels' argument structs; f32 kernels reinterpret)
+static double* xb(const acs_sim* s, uint32_t q) {
+    return reinterpret_cast<double*>(reinterpret_cast<char*>(s->xall) + (uint64_t)(q % s->H) * s->xstride * s->es);
+}
+// element k of a value buffer (byte arithmetic on the config's value size)
+static void* xat(const acs_sim* s, const void* base, uint64_t k) {
+    return const_cast<char*>(static_cast<const char*>(base)) + k * s->es;
+}
 
 static FinalizeArgs make_finalize(acs_sim* s, uint32_t r_next, const double2* partial, uint32_t nblk,
                                   bool init) {
@@ -239,6 +251,7 @@ static FinalizeArgs make_finalize(acs_sim* s, uint32_t r_next, const double2* pa
     f.trace_stride = (uint64_t)s->c.max_rounds + 1;
     f.n_done = s->n_done;
     f.init_mode = init ? 1u : 0u;
+    f.f32 = s->f32 ? 1u : 0u;
     return f;
 }
 
@@ -253,7 +266,7 @@ static uint64_t part_rows(const acs_sim* s, int p) {
 // holds the full x, so the initial honest min/max needs no exchange.
 static int init_state(acs_sim* s, uint32_t round) {
     HIP_TRY(hipMemsetAsync(s->n_done, 0, sizeof(uint32_t), s->stream));
-    HIP_TRY(launch_partials_from_x(xb(s, round), s->status, s->B, s->N, s->partial, s->nblk_init, s->stream));
+    HIP_TRY(launch_partials_from_x(xb(s, round), s->status, s->B, s->N, s->partial, s->nblk_init, s->f32, s->stream));
     const FinalizeArgs f = make_finalize(s, round, s->partial, s->nblk_init, true);
     HIP_TRY(launch_finalize(f, s->B, s->stream));
     HIP_TRY(hipMemcpyAsync(s->h_ndone, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
@@ -325,6 +338,7 @@ static RoundArgs round_args(acs_sim* s, uint32_t r) {
     a.r = r;
     a.nblk = s->nblk;
     a.mp = s->mp;
+    a.f32 = s->f32 ? 1u : 0u;
     return a;
 }
 
@@ -395,7 +409,8 @@ static int enqueue_round(acs_sim* s, uint32_t r) {
             for (int q = 0; q < s->nranks; ++q) {
                 if (q == p) continue;
                 double* dst = q == 0 ? s->x[o] : s->parts[q - 1].x[o];
-                HIP_TRY(hipMemcpyAsync(dst + r0, src + r0, nr * sizeof(double), hipMemcpyDeviceToDevice, s->stream));
+                HIP_TRY(hipMemcpyAsync(xat(s, dst, r0), xat(s, src, r0), nr * s->es, hipMemcpyDeviceToDevice,
+                                       s->stream));
             }
         }
         uint32_t nblk_live = 0;
@@ -415,7 +430,8 @@ static int enqueue_round(acs_sim* s, uint32_t r) {
     }
     if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
     double* xo = s->x[(r + 1) & 1u];
-    NCCL_TRY(ncclAllGather(xo + a.row0, xo, s->rows_per, ncclFloat64, s->comm, s->stream));
+    NCCL_TRY(ncclAllGather(xat(s, xo, a.row0), xo, s->rows_per, s->f32 ? ncclFloat32 : ncclFloat64, s->comm,
+                           s->stream));
     FinalizeArgs fold = make_finalize(s, r + 1, s->partial, a.nrows ? s->nblk : 0, false);
     fold.fold_out = s->gpart;
     HIP_TRY(launch_finalize(fold, s->B, s->stream));
@@ -592,7 +608,11 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     s->rows_per = partitioned ? ((s->N + nranks - 1) / nranks + 63) / 64 * 64 : s->N;
     s->Npad = partitioned ? s->rows_per * nranks : s->N;
 
-    if (cfg->topology == ACS_TOPO_COMPLETE && s->N <= kBatchedMaxN && cfg->delay_max == 0) {
+    s->f32 = cfg->dtype == ACS_F32;
+    s->es = s->f32 ? 4u : 8u;
+    // fp32 runs on the register and generic kernels; the batched, MFMA, dense and
+    // binned fast paths are fp64-only
+    if (cfg->topology == ACS_TOPO_COMPLETE && s->N <= kBatchedMaxN && cfg->delay_max == 0 && !s->f32) {
         s->path = PATH_BATCHED;
         s->kname = batched_small_name((uint32_t)s->N, cfg->rule, cfg->fault_model != ACS_FAULT_NONE);
         const char* env = getenv("ACSIM_MFMA");
@@ -600,7 +620,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
                   batched_mfma_supported((uint32_t)s->N, cfg->rule, cfg->fault_model != ACS_FAULT_NONE, cfg->mask_group,
                                          cfg->instance_offset);
         if (s->mfma) s->kname = "k_batched_mfma<v_mfma_f64_16x16x4>";
-    } else if (cfg->topology == ACS_TOPO_COMPLETE && !partitioned && cfg->delay_max == 0 &&
+    } else if (cfg->topology == ACS_TOPO_COMPLETE && !partitioned && cfg->delay_max == 0 && !s->f32 &&
                (s->B == 1 || (s->N <= kDensePersistMaxN && !env_off("ACSIM_DENSE_PERSIST"))) &&
                dense_supported(cfg->fault_model, cfg->byz_strategy, cfg->rule, s->mp.thr, s->N)) {
         s->path = PATH_DENSE;
@@ -635,7 +655,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         const char* env = getenv("ACSIM_BINNED");
         const bool allow = !(env && env[0] == '0');
         const uint32_t lv = s->path == PATH_REGULAR && s->d ? binned_levels(s->N, rows_local, s->d, bin_sa, nullptr) : 0;
-        s->binned = allow && s->path == PATH_REGULAR && cfg->delay_max == 0 && s->B == 1 && lv != 0 &&
+        s->binned = allow && !s->f32 && s->path == PATH_REGULAR && cfg->delay_max == 0 && s->B == 1 && lv != 0 &&
                     binned_supported(s->d, cfg->trim, cfg->rule) && rows_local * s->d < (1ull << 32);
         if (s->binned) {
             char nm[96];
@@ -670,9 +690,9 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     const uint64_t xlen = s->B * s->Npad;
     s->H = cfg->delay_max + 2;
     s->xstride = xlen + 2;   // +2: 16-byte tail reads (binned)
-    CREATE_TRY(hipMalloc(&s->xall, s->H * s->xstride * sizeof(double)));
-    s->x[0] = s->xall;
-    s->x[1] = s->xall + s->xstride;
+    CREATE_TRY(hipMalloc(&s->xall, s->H * s->xstride * s->es));
+    s->x[0] = xb(s, 0);
+    s->x[1] = xb(s, 1);
     CREATE_TRY(hipMalloc(&s->st, s->B * sizeof(InstState)));
     CREATE_TRY(hipMemsetAsync(s->st, 0, s->B * sizeof(InstState), s->stream));
     CREATE_TRY(hipMalloc(&s->partial, s->B * ncap * sizeof(double2)));
@@ -704,8 +724,8 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
             s->parts.resize(nranks - 1);
             for (int p = 1; p < nranks; ++p) {
                 Part& q = s->parts[p - 1];
-                CREATE_TRY(hipMalloc(&q.x[0], (xlen + 2) * sizeof(double)));
-                CREATE_TRY(hipMalloc(&q.x[1], (xlen + 2) * sizeof(double)));
+                CREATE_TRY(hipMalloc(&q.x[0], (xlen + 2) * s->es));
+                CREATE_TRY(hipMalloc(&q.x[1], (xlen + 2) * s->es));
                 CREATE_TRY(hipMalloc(&q.ell, words * sizeof(uint32_t)));
                 CREATE_TRY(hipMemsetAsync(q.ell, 0, words * sizeof(uint32_t), s->stream));
                 CREATE_TRY(build_rows(s, q.ell, p));
@@ -729,8 +749,9 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         CREATE_TRY(hipMemcpy(s->rowptr, h_rowptr, (s->N + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
         if (csr_nnz) CREATE_TRY(hipMemcpy(s->colidx, h_colidx, csr_nnz * sizeof(uint32_t), hipMemcpyHostToDevice));
     }
-    CREATE_TRY(launch_init_values(s->x[0], s->B, s->N, s->mp.key, cfg->instance_offset, s->stream));
-    for (Part& q : s->parts) CREATE_TRY(launch_init_values(q.x[0], s->B, s->N, s->mp.key, cfg->instance_offset, s->stream));
+    CREATE_TRY(launch_init_values(s->x[0], s->B, s->N, s->mp.key, cfg->instance_offset, s->f32, s->stream));
+    for (Part& q : s->parts)
+        CREATE_TRY(launch_init_values(q.x[0], s->B, s->N, s->mp.key, cfg->instance_offset, s->f32, s->stream));
 #undef CREATE_TRY
     if (comm_id) {
         ncclUniqueId id;
@@ -867,7 +888,7 @@ int acs_get_values(acs_sim* s, uint64_t b, void* out, uint64_t n) {
     InstState e;
     HIP_TRY(hipMemcpyAsync(&e, s->st + b, sizeof e, hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
-    HIP_TRY(hipMemcpyAsync(out, xb(s, e.rounds) + b * s->Npad, s->N * sizeof(double), hipMemcpyDeviceToHost,
+    HIP_TRY(hipMemcpyAsync(out, xat(s, xb(s, e.rounds), b * s->Npad), s->N * s->es, hipMemcpyDeviceToHost,
                            s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     return ACS_OK;
@@ -881,7 +902,7 @@ int acs_get_partition_values(acs_sim* s, int partition, void* out, uint64_t n) {
     HIP_TRY(hipMemcpyAsync(&e, s->st, sizeof e, hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     const double* src = partition == 0 ? s->x[e.rounds & 1u] : s->parts[partition - 1].x[e.rounds & 1u];
-    HIP_TRY(hipMemcpyAsync(out, src, s->N * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipMemcpyAsync(out, src, s->N * s->es, hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     return ACS_OK;
 }
@@ -932,15 +953,15 @@ int acs_set_state(acs_sim* s, uint32_t round, const void* x, uint64_t n) {
     if (!s || !x || n != s->B * s->N) return fail(ACS_EINVAL, "set_state needs B*N values");
     if (round > s->c.max_rounds) return fail(ACS_EINVAL, "round > max_rounds");
     HIP_TRY(hipSetDevice(s->device));
-    const double* hx = (const double*)x;
     for (uint64_t b = 0; b < s->B; ++b) {
+        const void* hb = xat(s, x, b * s->N);
         // every delay-history buffer restarts from x; one buffer when synchronous
         for (uint32_t q = 0; q < (s->c.delay_max ? s->H : 1u); ++q)
-            HIP_TRY(hipMemcpyAsync((s->c.delay_max ? s->xall + q * s->xstride : xb(s, round)) + b * s->Npad,
-                                   hx + b * s->N, s->N * sizeof(double), hipMemcpyHostToDevice, s->stream));
-        for (Part& q : s->parts)
-            HIP_TRY(hipMemcpyAsync(q.x[round & 1u] + b * s->Npad, hx + b * s->N, s->N * sizeof(double),
+            HIP_TRY(hipMemcpyAsync(xat(s, s->c.delay_max ? xb(s, q) : xb(s, round), b * s->Npad), hb, s->N * s->es,
                                    hipMemcpyHostToDevice, s->stream));
+        for (Part& q : s->parts)
+            HIP_TRY(hipMemcpyAsync(xat(s, q.x[round & 1u], b * s->Npad), hb, s->N * s->es, hipMemcpyHostToDevice,
+                                   s->stream));
     }
     return init_state(s, round);
 }

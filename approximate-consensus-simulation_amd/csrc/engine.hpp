@@ -49,6 +49,7 @@ struct RoundArgs {
     const double* xh;
     uint64_t xstride;
     uint32_t H, delay;        // delay = D (0: synchronous)
+    uint32_t f32;             // ACS_F32: x buffers hold binary32 values
 };
 
 struct FinalizeArgs {
@@ -58,6 +59,7 @@ struct FinalizeArgs {
     uint32_t r_next;          // rounds value after this step (or the resumed round in init mode)
     uint32_t max_rounds;
     uint32_t term_eps;        // 1: EPS termination
+    uint32_t f32;             // ACS_F32: spread = binary32(hi - lo)
     double eps;
     double* trace;            // nullptr if disabled
     uint64_t trace_stride;    // max_rounds + 1
@@ -81,7 +83,7 @@ struct BatchArgs {
 };
 
 // ---- setup kernels (setup.hip)
-hipError_t launch_init_values(double* x, uint64_t B, uint64_t N, Key key, uint64_t inst_offset,
+hipError_t launch_init_values(double* x, uint64_t B, uint64_t N, Key key, uint64_t inst_offset, bool f32,
                               hipStream_t s);
 hipError_t launch_build_ell(uint32_t* ell, uint64_t N, uint64_t row0, uint64_t nrows, uint32_t d, uint32_t dp,
                             const Feistel& f, hipStream_t s);
@@ -93,7 +95,7 @@ hipError_t build_fault_status(uint32_t* status, uint64_t B, uint64_t N, uint32_t
 
 // ---- spread / termination (reduce.hip)
 hipError_t launch_partials_from_x(const double* x, const uint32_t* status, uint64_t B, uint64_t N,
-                                  double2* partial, uint32_t nblk, hipStream_t s);
+                                  double2* partial, uint32_t nblk, bool f32, hipStream_t s);
 hipError_t launch_finalize(const FinalizeArgs& a, uint64_t B, hipStream_t s);
 
 // ---- round kernels

@@ -10,12 +10,13 @@ namespace acs {
 
 constexpr int kReduceBlock = 256;
 
-__global__ __launch_bounds__(kReduceBlock) void k_partials_from_x(const double* __restrict__ x,
+template <typename VT>
+__global__ __launch_bounds__(kReduceBlock) void k_partials_from_x(const VT* __restrict__ x,
                                                                   const uint32_t* __restrict__ status,
                                                                   uint64_t N, double2* partial,
                                                                   uint32_t nblk) {
     const uint32_t lb = blockIdx.y;
-    const double* xb = x + lb * N;
+    const VT* xb = x + lb * N;
     const uint32_t* sb = status ? status + lb * N : nullptr;
     const uint64_t per = (N + nblk - 1) / nblk;
     const uint64_t beg = (uint64_t)blockIdx.x * per;
@@ -23,7 +24,7 @@ __global__ __launch_bounds__(kReduceBlock) void k_partials_from_x(const double* 
     double mn = kInf, mx = -kInf;
     for (uint64_t i = beg + threadIdx.x; i < end; i += kReduceBlock) {
         if (sb && sb[i] != kHonest) continue;
-        const double v = xb[i];
+        const double v = (double)xb[i];
         mn = __builtin_fmin(mn, v);
         mx = __builtin_fmax(mx, v);
     }
@@ -72,7 +73,7 @@ __global__ __launch_bounds__(kReduceBlock) void k_finalize(const FinalizeArgs a)
             *a.fold_out = make_double2(-mn, mx);
             return;
         }
-        const double spread = mx - mn;
+        const double spread = a.f32 ? (double)(float)(mx - mn) : mx - mn;   // binary32 subtraction
         S->lo = mn;
         S->hi = mx;
         S->spread = spread;
@@ -87,9 +88,13 @@ __global__ __launch_bounds__(kReduceBlock) void k_finalize(const FinalizeArgs a)
 }
 
 hipError_t launch_partials_from_x(const double* x, const uint32_t* status, uint64_t B, uint64_t N,
-                                  double2* partial, uint32_t nblk, hipStream_t s) {
-    hipLaunchKernelGGL(k_partials_from_x, dim3(nblk, (unsigned)B), dim3(kReduceBlock), 0, s, x, status,
-                       N, partial, nblk);
+                                  double2* partial, uint32_t nblk, bool f32, hipStream_t s) {
+    if (f32)
+        hipLaunchKernelGGL(k_partials_from_x<float>, dim3(nblk, (unsigned)B), dim3(kReduceBlock), 0, s,
+                           reinterpret_cast<const float*>(x), status, N, partial, nblk);
+    else
+        hipLaunchKernelGGL(k_partials_from_x<double>, dim3(nblk, (unsigned)B), dim3(kReduceBlock), 0, s, x,
+                           status, N, partial, nblk);
     return hipGetLastError();
 }
 

@@ -9,21 +9,23 @@ constexpr double kInf = __builtin_huge_val();
 
 // §A.6 resolution of one non-self entry (i <- j, slot s, round r), given the sender's status
 // word, its value x_j, the receiver's x_i and the precomputed §A.5 drop decision.
-__device__ __forceinline__ double resolve_entry(const MsgParams& mp, uint32_t stj, double xj,
-                                                double xi, bool dropped, uint32_t b, uint32_t r,
-                                                uint32_t i, uint64_t s, double lo, double hi) {
+// VT = double, or float in fp32 mode.
+template <typename VT>
+__device__ __forceinline__ VT resolve_entry(const MsgParams& mp, uint32_t stj, VT xj, VT xi, bool dropped,
+                                            uint32_t b, uint32_t r, uint32_t i, uint64_t s, VT lo, VT hi) {
     const bool miss = dropped || crash_missing(mp, stj, b, r, s);
     if (miss) return xi;
-    if (stj == kByz) return byz_value(mp, b, r, i, s, lo, hi);
+    if (stj == kByz) return byz_value_t(mp, b, r, i, s, lo, hi);
     return xj;
 }
 
 // DESIGN.md §9 bounded delay: sender j's value as delivered on slot s in round r, given the
 // slot's DELAY draw w: x_j^{r - min(r, w mod (D + 1))}.
-__device__ __forceinline__ double delayed_x(const RoundArgs& a, uint32_t lb, uint32_t r, uint32_t w, uint64_t j) {
+template <typename VT = double>
+__device__ __forceinline__ VT delayed_x(const RoundArgs& a, uint32_t lb, uint32_t r, uint32_t w, uint64_t j) {
     uint32_t dl = w % (a.delay + 1);
     dl = dl < r ? dl : r;
-    return a.xh[(uint64_t)((r - dl) % a.H) * a.xstride + (uint64_t)lb * a.N + j];
+    return reinterpret_cast<const VT*>(a.xh)[(uint64_t)((r - dl) % a.H) * a.xstride + (uint64_t)lb * a.N + j];
 }
 
 __device__ __forceinline__ double wave_min(double v) {

@@ -11,7 +11,8 @@ namespace acs {
 
 constexpr int kGenericBlock = 256;
 
-__device__ __forceinline__ double block_tree_sum(double* w, uint32_t P) {
+template <typename VT>
+__device__ __forceinline__ VT block_tree_sum(VT* w, uint32_t P) {
     for (uint32_t s = P >> 1; s >= 1; s >>= 1) {
         for (uint32_t k = threadIdx.x; k < s; k += kGenericBlock) w[k] = w[k] + w[k + s];
         __syncthreads();
@@ -19,13 +20,14 @@ __device__ __forceinline__ double block_tree_sum(double* w, uint32_t P) {
     return w[0];
 }
 
-__device__ __forceinline__ void block_bitonic_sort(double* v, uint32_t P) {
+template <typename VT>
+__device__ __forceinline__ void block_bitonic_sort(VT* v, uint32_t P) {
     for (uint32_t k = 2; k <= P; k <<= 1) {
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
             for (uint32_t idx = threadIdx.x; idx < P; idx += kGenericBlock) {
                 const uint32_t ixj = idx ^ j;
                 if (ixj > idx) {
-                    const double p = v[idx], q = v[ixj];
+                    const VT p = v[idx], q = v[ixj];
                     const bool up = (idx & k) == 0;
                     if (up ? (q < p) : (p < q)) {
                         v[idx] = q;
@@ -38,16 +40,19 @@ __device__ __forceinline__ void block_bitonic_sort(double* v, uint32_t P) {
     }
 }
 
+// VT = double, or float in fp32 mode
+template <typename VT>
 __global__ __launch_bounds__(kGenericBlock) void k_round_generic(const RoundArgs a, uint32_t P) {
-    extern __shared__ __attribute__((aligned(16))) double sh[];  // [P] entries + [P] scratch
+    extern __shared__ __attribute__((aligned(16))) unsigned char sh_raw[];
+    VT* sh = reinterpret_cast<VT*>(sh_raw);   // [P] entries + [P] scratch
     const uint32_t lb = blockIdx.y, i = blockIdx.x;
     InstState* S = a.st + lb;
     if (S->done) return;
     const uint64_t N = a.N;
-    const double* __restrict__ x = a.xin + lb * N;
-    double* __restrict__ xo = a.xout + lb * N;
+    const VT* __restrict__ x = reinterpret_cast<const VT*>(a.xin) + lb * N;
+    VT* __restrict__ xo = reinterpret_cast<VT*>(a.xout) + lb * N;
     const uint32_t* stv = a.status ? a.status + lb * N : nullptr;
-    const double xi = x[i];
+    const VT xi = x[i];
     const uint32_t si = stv ? stv[i] : kHonest;
     const bool honest = si == kHonest;
     double2* part = a.partial + (uint64_t)lb * a.nblk + i;
@@ -68,12 +73,12 @@ __global__ __launch_bounds__(kGenericBlock) void k_round_generic(const RoundArgs
         rp = a.rowptr[i];
         m = (uint32_t)(a.rowptr[i + 1] - rp) + 1;
     }
-    const double lo = S->lo, hi = S->hi;
+    const VT lo = (VT)S->lo, hi = (VT)S->hi;
     const bool avg = a.rule == 0;
     for (uint32_t e = threadIdx.x; e < P; e += kGenericBlock) {
-        double v;
+        VT v;
         if (e >= m) {
-            v = avg ? 0.0 : kInf;
+            v = avg ? VT(0) : (VT)kInf;
         } else {
             uint32_t j;
             uint64_t slot;
@@ -97,16 +102,16 @@ __global__ __launch_bounds__(kGenericBlock) void k_round_generic(const RoundArgs
             } else {
                 const uint32_t stj = stv ? stv[j] : kHonest;
                 const bool dropped = mp.thr && draw(mp.key, kStreamDrop, bG, r, slot) < mp.thr;
-                const double xj = a.delay ? delayed_x(a, lb, r, draw(mp.key, kStreamDelay, b, r, slot), j) : x[j];
+                const VT xj = a.delay ? delayed_x<VT>(a, lb, r, draw(mp.key, kStreamDelay, b, r, slot), j) : x[j];
                 v = resolve_entry(mp, stj, xj, xi, dropped, b, r, i, slot, lo, hi);
             }
         }
         sh[e] = v;
     }
     __syncthreads();
-    double res;
+    VT res;
     if (avg) {
-        res = block_tree_sum(sh, P) / (double)m;
+        res = block_tree_sum(sh, P) / (VT)m;
     } else {
         block_bitonic_sort(sh, P);
         const uint32_t t = a.trim, nr = m - 2 * t;
@@ -124,26 +129,26 @@ __global__ __launch_bounds__(kGenericBlock) void k_round_generic(const RoundArgs
             const uint32_t wlo = nl < t ? nl : t, whi = ng < t ? ng : t, cnt = m - wlo - whi;
             uint32_t P2 = 1;
             while (P2 < cnt) P2 <<= 1;
-            double* w = sh + P;
-            for (uint32_t k = threadIdx.x; k < P2; k += kGenericBlock) w[k] = k < cnt ? sh[wlo + k] : 0.0;
+            VT* w = sh + P;
+            for (uint32_t k = threadIdx.x; k < P2; k += kGenericBlock) w[k] = k < cnt ? sh[wlo + k] : VT(0);
             __syncthreads();
-            res = block_tree_sum(w, P2) / (double)cnt;
+            res = block_tree_sum(w, P2) / (VT)cnt;
         } else if (a.rule == 2) {
-            res = (sh[t] + sh[m - t - 1]) * 0.5;
+            res = (sh[t] + sh[m - t - 1]) * VT(0.5);
         } else {
             const uint32_t step = a.rule == 3 ? t : 1;
             const uint32_t cnt = a.rule == 3 ? (nr + t - 1) / t : nr;
             uint32_t P2 = 1;
             while (P2 < cnt) P2 <<= 1;
-            double* w = sh + P;
-            for (uint32_t k = threadIdx.x; k < P2; k += kGenericBlock) w[k] = k < cnt ? sh[t + k * step] : 0.0;
+            VT* w = sh + P;
+            for (uint32_t k = threadIdx.x; k < P2; k += kGenericBlock) w[k] = k < cnt ? sh[t + k * step] : VT(0);
             __syncthreads();
-            res = block_tree_sum(w, P2) / (double)cnt;
+            res = block_tree_sum(w, P2) / (VT)cnt;
         }
     }
     if (threadIdx.x == 0) {
         xo[i] = res;
-        *part = honest ? make_double2(res, res) : make_double2(kInf, -kInf);
+        *part = honest ? make_double2((double)res, (double)res) : make_double2(kInf, -kInf);
     }
 }
 
@@ -151,17 +156,20 @@ hipError_t launch_round_generic(const RoundArgs& a, uint64_t B, hipStream_t s) {
     uint32_t P = 1;
     while (P < a.m) P <<= 1;
     if (P > kGenericMaxM) return hipErrorNotSupported;
-    const size_t lds = 2 * (size_t)P * sizeof(double);
+    const size_t lds = 2 * (size_t)P * (a.f32 ? sizeof(float) : sizeof(double));
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_round_generic,
+        hipError_t e = hipFuncSetAttribute((const void*)k_round_generic<double>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)(2 * kGenericMaxM * sizeof(double)));
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     const dim3 grid((unsigned)a.N, (unsigned)B);
-    hipLaunchKernelGGL(k_round_generic, grid, dim3(kGenericBlock), lds, s, a, P);
+    if (a.f32)
+        hipLaunchKernelGGL(k_round_generic<float>, grid, dim3(kGenericBlock), lds, s, a, P);
+    else
+        hipLaunchKernelGGL(k_round_generic<double>, grid, dim3(kGenericBlock), lds, s, a, P);
     return hipGetLastError();
 }
 

@@ -17,7 +17,8 @@
 
 namespace acs {
 
-template <int D, int T, bool CLEAN, bool WMSR = false>
+// VT = double, or float in fp32 mode (4-byte gathers, binary32 rule arithmetic).
+template <int D, int T, bool CLEAN, bool WMSR = false, typename VT = double>
 __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs a) {
     static_assert(D % 4 == 0, "compiled degrees are multiples of 4");
     constexpr int M = D + 1;
@@ -27,15 +28,15 @@ __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs
     if (S->done) return;  // device-side early exit (uniform per block)
 
     const uint64_t N = a.N;
-    const double* __restrict__ x = a.xin + lb * N;
-    double* __restrict__ xo = a.xout + lb * N;
+    const VT* __restrict__ x = reinterpret_cast<const VT*>(a.xin) + lb * N;
+    VT* __restrict__ xo = reinterpret_cast<VT*>(a.xout) + lb * N;
     const uint32_t li = blockIdx.x * kRegularBlock + threadIdx.x;   // local row (ELL row)
     const uint32_t i = (uint32_t)a.row0 + li;                        // global receiver id
 
-    double mn = kInf, mx = -kInf;
+    double mn = kInf, mx = -kInf;   // exact for binary32 values too
     if (li < a.nrows && i < N) {
-        const double xi = x[i];
-        double res = xi;
+        const VT xi = x[i];
+        VT res = xi;
         bool honest = true, active = true;
         const uint32_t* stv = nullptr;   // null: loss only, no fault schedule
         if constexpr (!CLEAN) {
@@ -58,7 +59,7 @@ __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs
                 col[4 * q + 2] = c.z;
                 col[4 * q + 3] = c.w;
             }
-            double v[M];
+            VT v[M];
             v[0] = xi;
             if constexpr (CLEAN) {
 #pragma unroll
@@ -67,9 +68,9 @@ __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs
                 const MsgParams& mp = a.mp;
                 const uint32_t b = (uint32_t)(mp.inst_offset + lb);
                 const uint32_t bG = b - b % mp.mask_group;
-                const double lo = S->lo, hi = S->hi;
+                const VT lo = (VT)S->lo, hi = (VT)S->hi;
                 const uint32_t r = a.r;
-                double xj[D];
+                VT xj[D];
                 uint32_t sj[D];
                 // all gathers first, unconditionally (the branch is uniform and hoisted)
                 if (a.delay) {   // bounded delay: one DELAY Philox call per 4 slots, history gathers
@@ -79,7 +80,7 @@ __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs
 #pragma unroll
                         for (int e = 0; e < 4; ++e) {
                             const int t = 4 * q + e;
-                            xj[t] = delayed_x(a, lb, r, wd.v[e], col[t]);
+                            xj[t] = delayed_x<VT>(a, lb, r, wd.v[e], col[t]);
                             sj[t] = stv ? stv[col[t]] : kHonest;
                         }
                     }
@@ -122,6 +123,19 @@ __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs
     block_minmax_store<kRegularBlock>(mn, mx, a.partial + (uint64_t)lb * a.nblk + blockIdx.x);
 }
 
+template <int D, int T, typename VT>
+static void launch_regular_t(const RoundArgs& a, dim3 grid, dim3 block, bool clean, hipStream_t s) {
+    const bool w = a.rule == 4;
+    if (clean && w)
+        hipLaunchKernelGGL((k_round_regular<D, T, true, true, VT>), grid, block, 0, s, a);
+    else if (clean)
+        hipLaunchKernelGGL((k_round_regular<D, T, true, false, VT>), grid, block, 0, s, a);
+    else if (w)
+        hipLaunchKernelGGL((k_round_regular<D, T, false, true, VT>), grid, block, 0, s, a);
+    else
+        hipLaunchKernelGGL((k_round_regular<D, T, false, false, VT>), grid, block, 0, s, a);
+}
+
 // ---------------------------------------------------------------------------- dispatch
 // (D, T) pairs compiled into the register path; anything else uses the generic kernel.
 #define ACS_REGULAR_VARIANTS(X) \
@@ -157,15 +171,10 @@ hipError_t launch_round_regular(const RoundArgs& a, uint64_t B, bool clean, hipS
     const dim3 block(kRegularBlock);
 #define X(DD, TT)                                                                         \
     if (a.d == DD && a.trim == TT) {                                                      \
-        const bool w_ = a.rule == 4;                                                      \
-        if (clean && w_)                                                                  \
-            hipLaunchKernelGGL((k_round_regular<DD, TT, true, true>), grid, block, 0, s, a); \
-        else if (clean)                                                                   \
-            hipLaunchKernelGGL((k_round_regular<DD, TT, true>), grid, block, 0, s, a);    \
-        else if (w_)                                                                      \
-            hipLaunchKernelGGL((k_round_regular<DD, TT, false, true>), grid, block, 0, s, a); \
+        if (a.f32)                                                                        \
+            launch_regular_t<DD, TT, float>(a, grid, block, clean, s);                     \
         else                                                                              \
-            hipLaunchKernelGGL((k_round_regular<DD, TT, false>), grid, block, 0, s, a);   \
+            launch_regular_t<DD, TT, double>(a, grid, block, clean, s);                    \
         return hipGetLastError();                                                         \
     }
     ACS_REGULAR_VARIANTS(X)

@@ -13,10 +13,10 @@ namespace acs {
 // The window start is a runtime value in [0, T]; zero padding past the window leaves the
 // stride-halving sum unchanged (no -0.0 values), so the compile-time tree over next_pow2(M)
 // equals the spec's tree over next_pow2(window).
-template <int D, int T>
-__device__ __forceinline__ double wmsr_reg(double (&v)[D + 1]) {
+template <int D, int T, typename VT>
+__device__ __forceinline__ VT wmsr_reg(VT (&v)[D + 1]) {
     constexpr int M = D + 1;
-    const double xi = v[0];
+    const VT xi = v[0];
     select_sort<M>(v);
     uint32_t nl = 0, ng = 0;
 #pragma unroll
@@ -26,39 +26,39 @@ __device__ __forceinline__ double wmsr_reg(double (&v)[D + 1]) {
     }
     const uint32_t lo = nl < (uint32_t)T ? nl : (uint32_t)T, hi = ng < (uint32_t)T ? ng : (uint32_t)T;
     const uint32_t nw = M - lo - hi;
-    double w[M];
+    VT w[M];
 #pragma unroll
     for (int k = 0; k < M; ++k) {
-        double s = v[k];
+        VT s = v[k];
 #pragma unroll
         for (int q = 1; q <= T; ++q)
             if (k + q < M && lo == (uint32_t)q) s = v[k + q];
-        w[k] = (uint32_t)k < nw ? s : 0.0;
+        w[k] = (uint32_t)k < nw ? s : VT(0);
     }
-    return tree_sum_const<M>(w) / (double)nw;
+    return tree_sum_const<M>(w) / (VT)nw;
 }
 
 // WMSR = true instantiates the W-MSR rule only (a separate kernel instantiation, so the other
 // rules' kernels carry none of its registers).
-template <int D, int T, bool WMSR = false>
-__device__ __forceinline__ double apply_rule_reg(uint32_t rule, double (&v)[D + 1]) {
+template <int D, int T, bool WMSR = false, typename VT>
+__device__ __forceinline__ VT apply_rule_reg(uint32_t rule, VT (&v)[D + 1]) {
     constexpr int M = D + 1;
     if constexpr (WMSR) {
         return wmsr_reg<D, T>(v);
     }
     if constexpr (T == 0) {
-        if (rule == 0) return tree_sum_const<M>(v) / (double)M;   // AVERAGE: entry order
+        if (rule == 0) return tree_sum_const<M>(v) / (VT)M;       // AVERAGE: entry order
     }
     select_sort<M, T, M - T>(v);
     constexpr int NR = M - 2 * T;
-    if (rule == 2) return (v[T] + v[M - T - 1]) * 0.5;                // MIDPOINT
+    if (rule == 2) return (v[T] + v[M - T - 1]) * VT(0.5);            // MIDPOINT
     if constexpr (T >= 1) {
         if (rule == 3) {                                             // DLPSW: R[0], R[T], ...
             constexpr int NQ = (NR + T - 1) / T;
-            return tree_sum_const<NQ, T, T>(v) / (double)NQ;
+            return tree_sum_const<NQ, T, T>(v) / (VT)NQ;
         }
     }
-    return tree_sum_const<NR, T>(v) / (double)NR;                    // TRIMMED_MEAN
+    return tree_sum_const<NR, T>(v) / (VT)NR;                        // TRIMMED_MEAN
 }
 
 }  // namespace acs

@@ -10,14 +10,19 @@ namespace acs {
 
 // §A.2: x_i^0 = u53(draw(INIT,b,0,2i), draw(INIT,b,0,2i+1)); both words come from one Philox
 // call (counter (2i)>>2 = i>>1, words 2(i&1) and 2(i&1)+1).
-__global__ __launch_bounds__(256) void k_init_values(double* x, uint64_t N, Key key, uint64_t inst_offset) {
+// fp32 mode: x_i = (draw(INIT, b, 0, 2i) >> 8) * 2^-24, exact in binary32
+__global__ __launch_bounds__(256) void k_init_values(double* x, uint64_t N, Key key, uint64_t inst_offset,
+                                                     uint32_t f32) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const uint32_t lb = blockIdx.y;
     if (i >= N) return;
     const uint32_t b = (uint32_t)(inst_offset + lb);
     const U4 w = philox10((uint32_t)(i >> 1), 0u, b, kStreamInit, key);
     const uint32_t sel = (uint32_t)((i & 1u) << 1);
-    x[lb * N + i] = u53(pick(w, sel), pick(w, sel + 1));
+    if (f32)
+        reinterpret_cast<float*>(x)[lb * N + i] = (float)(pick(w, sel) >> 8) * 0x1p-24f;
+    else
+        x[lb * N + i] = u53(pick(w, sel), pick(w, sel + 1));
 }
 
 // §A.3: column t of node i is π_{t/2}(i) (t even) or π_{t/2}^{-1}(i) (t odd).  Builds the rows
@@ -100,10 +105,10 @@ struct SegOffset {
     __host__ __device__ uint64_t operator()(uint64_t b) const { return b * N; }
 };
 
-hipError_t launch_init_values(double* x, uint64_t B, uint64_t N, Key key, uint64_t inst_offset,
+hipError_t launch_init_values(double* x, uint64_t B, uint64_t N, Key key, uint64_t inst_offset, bool f32,
                               hipStream_t s) {
     hipLaunchKernelGGL(k_init_values, dim3((unsigned)((N + 255) / 256), (unsigned)B), dim3(256), 0, s, x, N,
-                       key, inst_offset);
+                       key, inst_offset, f32 ? 1u : 0u);
     return hipGetLastError();
 }
 

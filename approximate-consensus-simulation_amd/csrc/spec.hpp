@@ -162,6 +162,25 @@ ACS_HD double byz_value(const MsgParams& p, uint32_t b, uint32_t r, uint32_t i, 
     return (lo - p.delta) + u * width;
 }
 
+// DESIGN.md §9 fp32 mode: Δ and c rounded to binary32 once; RANDOM uses u24 = (draw(BYZ, b, r,
+// 2s) >> 8) * 2^-24; every step is a binary32 operation in the order written (no FMA).
+ACS_HD float byz_value_f32(const MsgParams& p, uint32_t b, uint32_t r, uint32_t i, uint64_t s, float lo,
+                           float hi) {
+    const float dl = (float)p.delta;
+    if (p.byz == 0) return (i & 1u) == 0 ? hi + dl : lo - dl;   // SPLIT
+    if (p.byz == 2) return (float)p.bconst + 0.0f;               // CONSTANT (canonical +0)
+    const float u = (float)(draw(p.key, kStreamByz, b, r, 2 * s) >> 8) * 0x1p-24f;
+    const float width = (hi - lo) + 2.0f * dl;
+    return (lo - dl) + u * width;
+}
+ACS_HD double byz_value_t(const MsgParams& p, uint32_t b, uint32_t r, uint32_t i, uint64_t s, double lo,
+                          double hi) {
+    return byz_value(p, b, r, i, s, lo, hi);
+}
+ACS_HD float byz_value_t(const MsgParams& p, uint32_t b, uint32_t r, uint32_t i, uint64_t s, float lo, float hi) {
+    return byz_value_f32(p, b, r, i, s, lo, hi);
+}
+
 // §A.4 crash semantics of a sender with status word st in round r: true = message missing.
 ACS_HD bool crash_missing(const MsgParams& p, uint32_t st, uint32_t b, uint32_t r, uint64_t s) {
     if (st >= kByz) return false;  // honest or Byzantine

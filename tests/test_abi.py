@@ -107,11 +107,18 @@ def test_cpu_backend_is_not_a_product_path(acsim_lib):
         acsim.Simulator("cfg1", backend="cpu")
 
 
-def test_f32_reported_unsupported(acsim_lib):
-    c = preset("cfg1", dtype="f32").to_c()
+def test_dtype_validation(acsim_lib, oracle_mod):
+    """fp32 is a product dtype; its Byzantine parameters must fit binary32 and an
+    unknown dtype is rejected — the same verdicts from the library and the oracle."""
     h = C.c_void_p()
     devs = (C.c_int * 1)(0)
-    assert acsim_lib.acs_create(C.byref(c), _abi.BACKEND_HIP, devs, 1, C.byref(h)) == _abi.EUNSUPPORTED
+    bad = preset("cfg4_byz", n_nodes=4096, dtype="f32", byz_delta=1e31)
+    assert oracle_mod.validate(bad) == _abi.EINVAL
+    assert acsim_lib.acs_create(C.byref(bad.to_c()), _abi.BACKEND_HIP, devs, 1, C.byref(h)) == _abi.EINVAL
+    c = preset("cfg1").to_c()
+    c.dtype = 7
+    assert acsim_lib.acs_create(C.byref(c), _abi.BACKEND_HIP, devs, 1, C.byref(h)) == _abi.EINVAL
+    assert oracle_mod.validate(preset("cfg4", dtype="f32")) == 0
 
 
 def test_presets_valid(oracle_mod):

@@ -1,0 +1,82 @@
+"""fp32 mode on the GPU against the oracle: binary32 values and arithmetic, same
+seeds.  Bar: bit-exact final values, spread traces and rounds-to-convergence (every kernel does
+IEEE binary32 adds / divides without FMA in the spec's order, so there is nothing to tolerate).
+"""
+import numpy as np
+import pytest
+
+import acsim
+from acsim.config import Config, preset
+from test_gpu_parity import assert_same, run_both
+
+pytestmark = pytest.mark.gpu
+
+CASES = {
+    # per-lane register kernel, clean (the cfg4 shape in binary32)
+    "cfg4_shaped": preset("cfg4_eps", n_nodes=8192, dtype="f32", eps=1e-6, trace_spread=True),
+    # register kernel, Byzantine RANDOM + loss
+    "regular_byzrandom_drop": Config(n_nodes=3000, topology="regular", degree=16, rule="trimmed", trim=5,
+                                     fault_model="byzantine", n_faulty=60, byz_strategy="random",
+                                     byz_delta=0.05, loss_p=0.1, eps=1e-6, max_rounds=300, seed=3,
+                                     trace_spread=True, dtype="f32"),
+    # register kernel, W-MSR + crash
+    "regular_wmsr_crash": Config(n_nodes=2000, topology="regular", degree=8, rule="wmsr", trim=2,
+                                 fault_model="crash", n_faulty=40, crash_window=4, eps=1e-6,
+                                 max_rounds=300, seed=5, trace_spread=True, dtype="f32"),
+    # register kernel, bounded delay + Byzantine CONSTANT + loss
+    "regular_delay_const": Config(n_nodes=1500, topology="regular", degree=8, rule="trimmed", trim=2,
+                                  fault_model="byzantine", n_faulty=10, byz_strategy="constant",
+                                  byz_const=0.7, loss_p=0.05, delay_max=3, eps=1e-6, max_rounds=300,
+                                  seed=16, trace_spread=True, dtype="f32"),
+    # generic kernel: complete graph, midpoint, crash + loss (cfg1-like)
+    "complete_mid_crash_drop": Config(n_nodes=50, topology="complete", rule="midpoint", trim=4,
+                                      fault_model="crash", n_faulty=6, crash_window=3, loss_p=0.15,
+                                      eps=1e-6, max_rounds=200, seed=21, trace_spread=True, dtype="f32"),
+    # generic kernel: batched averaging instances with grouped drop masks (cfg3-like)
+    "complete_avg_batched": Config(n_nodes=64, n_instances=40, topology="complete", rule="average",
+                                   loss_p=0.2, mask_group=4, eps=1e-6, max_rounds=100, seed=2,
+                                   dtype="f32"),
+    # generic kernel: Byzantine SPLIT trimmed mean on a complete graph (cfg2-like, smaller)
+    "complete_trimmed_split": Config(n_nodes=256, topology="complete", rule="trimmed", trim=85,
+                                     fault_model="byzantine", n_faulty=85, byz_strategy="split",
+                                     eps=1e-6, max_rounds=2000, seed=0, trace_spread=True, dtype="f32"),
+    # odd (d, t): generic kernel on a random-regular graph, DLPSW
+    "regular_generic_dlpsw": Config(n_nodes=1000, topology="regular", degree=10, rule="dlpsw", trim=3,
+                                    eps=1e-6, max_rounds=300, seed=9, trace_spread=True, dtype="f32"),
+}
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_f32_matches_oracle(oracle_mod, name):
+    cfg = CASES[name]
+    g, o = run_both(oracle_mod, cfg)
+    assert g["x"].dtype == np.float32 and o["x"].dtype == np.float32
+    assert_same(g, o)
+    assert int(g["rounds"].max()) > 2
+
+
+def test_f32_resume_and_chunks(oracle_mod):
+    cfg = preset("cfg4_eps", n_nodes=4096, loss_p=0.1, dtype="f32", eps=1e-6)
+    with acsim.Simulator(cfg, device=0) as g, oracle_mod.OracleSimulator(cfg, threads=8) as o:
+        g.round(3)
+        o.round(3)
+        x3 = g.values(0)
+        assert np.array_equal(x3.view(np.uint32), o.values(0).view(np.uint32))
+        g.run()
+        o.run()
+        final = g.values(0)
+        assert np.array_equal(final.view(np.uint32), o.values(0).view(np.uint32))
+    with acsim.Simulator(cfg, device=0) as h:
+        h.set_state(3, x3)
+        h.run()
+        assert np.array_equal(h.values(0).view(np.uint32), final.view(np.uint32))
+
+
+@pytest.mark.parametrize("parts", [2, 3])
+def test_f32_virtual_partitions(oracle_mod, parts):
+    cfg = preset("cfg4_eps", n_nodes=6000, dtype="f32", eps=1e-6)
+    with acsim.Simulator(cfg, device=0) as ref, acsim.Simulator(cfg, partitions=parts) as p:
+        ref.run()
+        p.run()
+        assert np.array_equal(ref.rounds(), p.rounds())
+        assert np.array_equal(ref.values(0).view(np.uint32), p.values(0).view(np.uint32))
