@@ -648,22 +648,27 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     // one or two exchange levels (faults and loss are resolved in phase B from tagged values and
     // slot-order draws); ACSIM_BINNED=0 forces the per-lane kernel and ACSIM_BIN_SA sets the
     // source block size (tests use small blocks on small graphs)
-    uint32_t bin_sa = 16384;
+    // (128 KiB of LDS per phase-A source block: 16 Ki fp64 or 32 Ki fp32 senders)
+    const uint32_t sa_max = s->f32 ? 32768u : 16384u;
+    uint32_t bin_sa = sa_max;
     if (const char* v = getenv("ACSIM_BIN_SA")) bin_sa = (uint32_t)strtoul(v, nullptr, 10);
-    if (bin_sa < 64 || bin_sa > 16384 || (bin_sa & (bin_sa - 1))) bin_sa = 16384;
+    if (bin_sa < 64 || bin_sa > sa_max || (bin_sa & (bin_sa - 1))) bin_sa = sa_max;
     {
         const char* env = getenv("ACSIM_BINNED");
         const bool allow = !(env && env[0] == '0');
         const uint32_t lv = s->path == PATH_REGULAR && s->d ? binned_levels(s->N, rows_local, s->d, bin_sa, nullptr) : 0;
-        s->binned = allow && !s->f32 && s->path == PATH_REGULAR && cfg->delay_max == 0 && s->B == 1 && lv != 0 &&
+        s->binned = allow && (!s->f32 || (s->clean && lv == 1)) && s->path == PATH_REGULAR && cfg->delay_max == 0 &&
+                    s->B == 1 && lv != 0 &&
                     binned_supported(s->d, cfg->trim, cfg->rule) && rows_local * s->d < (1ull << 32);
         if (s->binned) {
             char nm[96];
             snprintf(nm, sizeof nm, "k_bin_scatter+%sk_bin_gather<%u,%u%s>%s", lv == 2 ? "k_bin_regroup+" : "", s->d,
-                     cfg->trim, s->clean ? "" : ",faulty", cfg->fault_model != ACS_FAULT_NONE ? "+k_bin_tag" : "");
+                     cfg->trim, s->clean ? "" : ",faulty",
+                     cfg->fault_model != ACS_FAULT_NONE ? "+k_bin_tag" : "");
             s->kname = nm;
         }
     }
+    if (s->f32) s->kname += " [f32]";
     s->nblk = s->path == PATH_REGULAR ? (uint32_t)((rows_local + kRegularBlock - 1) / kRegularBlock)
             : s->path == PATH_GENERIC ? (uint32_t)s->N
             : s->path == PATH_DENSE   ? dense_nblk(s->N)
@@ -689,7 +694,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     CREATE_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     const uint64_t xlen = s->B * s->Npad;
     s->H = cfg->delay_max + 2;
-    s->xstride = xlen + 2;   // +2: 16-byte tail reads (binned)
+    s->xstride = xlen + 4;   // +4 elements: 16-byte tail reads (binned phase A staging)
     CREATE_TRY(hipMalloc(&s->xall, s->H * s->xstride * s->es));
     s->x[0] = xb(s, 0);
     s->x[1] = xb(s, 1);
@@ -716,7 +721,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         CREATE_TRY(build_rows(s, s->ell, partitioned ? rank : 0));
         if (s->binned) {   // the plan replaces the ELL in the round loop
             const uint64_t nr = partitioned ? part_rows(s, rank) : s->N;
-            if (nr) CREATE_TRY(binned_build(s->bin, s->ell, s->N, nr, s->d, s->dp, bin_sa, tagged, s->stream));
+            if (nr) CREATE_TRY(binned_build(s->bin, s->ell, s->N, nr, s->d, s->dp, bin_sa, tagged, s->f32, s->stream));
             (void)hipFree(s->ell);
             s->ell = nullptr;
         }
@@ -724,14 +729,14 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
             s->parts.resize(nranks - 1);
             for (int p = 1; p < nranks; ++p) {
                 Part& q = s->parts[p - 1];
-                CREATE_TRY(hipMalloc(&q.x[0], (xlen + 2) * s->es));
-                CREATE_TRY(hipMalloc(&q.x[1], (xlen + 2) * s->es));
+                CREATE_TRY(hipMalloc(&q.x[0], (xlen + 4) * s->es));
+                CREATE_TRY(hipMalloc(&q.x[1], (xlen + 4) * s->es));
                 CREATE_TRY(hipMalloc(&q.ell, words * sizeof(uint32_t)));
                 CREATE_TRY(hipMemsetAsync(q.ell, 0, words * sizeof(uint32_t), s->stream));
                 CREATE_TRY(build_rows(s, q.ell, p));
                 if (s->binned) {
                     const uint64_t nr = part_rows(s, p);
-                    if (nr) CREATE_TRY(binned_build(q.bin, q.ell, s->N, nr, s->d, s->dp, bin_sa, tagged, s->stream));
+                    if (nr) CREATE_TRY(binned_build(q.bin, q.ell, s->N, nr, s->d, s->dp, bin_sa, tagged, s->f32, s->stream));
                     (void)hipFree(q.ell);
                     q.ell = nullptr;
                 }

@@ -116,6 +116,7 @@ constexpr uint32_t kRegularBlock = 256;
 constexpr uint32_t kBinSB = 256;        // receivers per phase-B workgroup (one lane each)
 struct BinnedPlan {
     uint32_t D = 0, SA = 0, P = 0, Q = 0, levels = 0, PK = 0, ngroups = 0, nrun = 0, mcap = 0;
+    bool f32 = false;                   // fp32 plan (float stage, runs padded to 4 elements)
     uint32_t segs = 0, chunk = 0;       // phase-A workgroups per source block, deliveries per workgroup
     uint64_t E = 0;                     // deliveries = local rows * D
     uint64_t Ep1 = 0, Ep2 = 0;          // padded stage lengths
@@ -136,7 +137,7 @@ uint32_t binned_levels(uint64_t N, uint64_t NR, uint32_t d, uint32_t sa, uint32_
 // Builds the plan from the ELL of the NR local rows (sorted or spec order; slot-dependent configs
 // need spec order); sa = source block size; tagged: the config has a fault schedule.
 hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t NR, uint32_t d, uint32_t dp,
-                        uint32_t sa, bool tagged, hipStream_t s);
+                        uint32_t sa, bool tagged, bool f32, hipStream_t s);
 void binned_free(BinnedPlan& p);
 // clean: no slot-dependent decision (selects the plain phase-B instantiation)
 hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool clean, hipStream_t s);

@@ -47,22 +47,28 @@ constexpr uint32_t kBinMCap = 19456;   // phase-M LDS image capacity (elements, 
 // Stream [p0, p1) of an index stream: out[p] = lds[idx[p]].  Super-steps of 512 positions per
 // wave; instruction q of a lane covers positions q*128 + 2*lane, +1 (one u32 of two indices, one
 // 16-byte store), so every wave-instruction reads 256 B and writes 1 KiB contiguously.
-__device__ __forceinline__ void bin_stream(const double* lx, const uint16_t* __restrict__ idx, double* __restrict__ out,
+__device__ __forceinline__ double2 bin_pair(double a, double b) { return make_double2(a, b); }
+__device__ __forceinline__ float2 bin_pair(float a, float b) { return make_float2(a, b); }
+
+// VT = double, or float for fp32 plans (the instruction's store is then 8 bytes)
+template <typename VT = double>
+__device__ __forceinline__ void bin_stream(const VT* lx, const uint16_t* __restrict__ idx, VT* __restrict__ out,
                                            uint64_t p0, uint64_t p1) {
+    using V2 = decltype(bin_pair(VT(0), VT(0)));
     constexpr uint32_t SUP = kBinA / 64 * 512, SUPW = SUP / 2;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint64_t p = p0;
     if ((p0 & 1) == 0) {
         const uint64_t nsup = (p1 - p0) / SUP;
         const uint32_t* ip = reinterpret_cast<const uint32_t*>(idx + p0) + w * 256 + lane;
-        double2* op = reinterpret_cast<double2*>(out + p0) + w * 256 + lane;
+        V2* op = reinterpret_cast<V2*>(out + p0) + w * 256 + lane;
 #pragma unroll 4
         for (uint64_t k = 0; k < nsup; ++k) {
             uint32_t c[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) c[q] = __builtin_nontemporal_load(ip + k * SUPW + q * 64);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) op[k * SUPW + q * 64] = make_double2(lx[c[q] & 0xFFFFu], lx[c[q] >> 16]);
+            for (int q = 0; q < 4; ++q) op[k * SUPW + q * 64] = bin_pair(lx[c[q] & 0xFFFFu], lx[c[q] >> 16]);
         }
         p = p0 + nsup * SUP;
     }
@@ -73,8 +79,11 @@ __device__ __forceinline__ void bin_stream(const double* lx, const uint16_t* __r
 // image; run k ends where run k+1's image begins) into LDS by 16-byte LDS-DMA.  Every run is
 // padded to an even length, so starts are 16-byte aligned on both sides.  Descriptors are fetched
 // one per lane, 64 at a time, and broadcast with readlane: no run waits on a dependent load.
+// Runs are padded to EPU = 16 / sizeof(VT) elements (2 for fp64, 4 for fp32).
+template <typename VT = double>
 __device__ __forceinline__ void bin_dma_runs(const uint2* __restrict__ tb, uint32_t r0, uint32_t r1,
-                                             const double* __restrict__ src, double* dst) {
+                                             const VT* __restrict__ src, VT* dst) {
+    constexpr uint32_t EPU = 16 / sizeof(VT);
     const uint32_t lane = threadIdx.x & 63;
     const uint4* s16 = reinterpret_cast<const uint4*>(src);
     uint4* d16 = reinterpret_cast<uint4*>(dst);
@@ -89,9 +98,9 @@ __device__ __forceinline__ void bin_dma_runs(const uint2* __restrict__ tb, uint3
         for (uint32_t k = 0; k < ng; ++k) {
             const uint32_t so = __builtin_amdgcn_readlane(dsc.x, k);
             const uint32_t pre = __builtin_amdgcn_readlane(dsc.y, k);
-            const uint32_t n16 = (__builtin_amdgcn_readlane(nxt, k) - pre) >> 1;   // 16-byte units
-            const uint4* sp = s16 + (so >> 1) + lane;
-            uint4* dp = d16 + (pre >> 1);
+            const uint32_t n16 = (__builtin_amdgcn_readlane(nxt, k) - pre) / EPU;   // 16-byte units
+            const uint4* sp = s16 + so / EPU + lane;
+            uint4* dp = d16 + pre / EPU;
             for (uint32_t o = 0; o < n16; o += 64)
                 if (o + lane < n16) __builtin_amdgcn_global_load_lds(sp + o, dp + o, 16, 0, 0);
         }
@@ -99,11 +108,13 @@ __device__ __forceinline__ void bin_dma_runs(const uint2* __restrict__ tb, uint3
 }
 
 // ------------------------------------------------------------------------------ phase A
-__global__ __launch_bounds__(kBinA) void k_bin_scatter(const double* __restrict__ x, const uint16_t* __restrict__ idxA,
-                                                     const uint64_t* __restrict__ aoff, double* __restrict__ stage,
+template <typename VT = double>
+__global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x, const uint16_t* __restrict__ idxA,
+                                                     const uint64_t* __restrict__ aoff, VT* __restrict__ stage,
                                                      const InstState* __restrict__ st, uint64_t N, uint32_t SA,
                                                      uint32_t segs, uint32_t chunk) {
-    extern __shared__ double lx[];
+    extern __shared__ __attribute__((aligned(16))) unsigned char lx_raw[];
+    VT* lx = reinterpret_cast<VT*>(lx_raw);
     if (st->done) return;
     const uint32_t a = blockIdx.x / segs, sg = blockIdx.x % segs;
     const uint64_t pa1 = aoff[a + 1];
@@ -114,7 +125,8 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const double* __restrict_
     const uint32_t n = (uint32_t)(N - base < SA ? N - base : SA);
     {   // x block -> LDS by LDS-DMA, 16 B per lane (x is allocated with spare elements, so the
         // last odd element's pair never reads past the buffer)
-        const uint32_t n16 = (n + 1) / 2;
+        constexpr uint32_t EPU = 16 / sizeof(VT);
+        const uint32_t n16 = (n + EPU - 1) / EPU;
         const uint4* xs = reinterpret_cast<const uint4*>(x + base) + threadIdx.x;
         uint4* ld = reinterpret_cast<uint4*>(lx) + (threadIdx.x & ~63u);
         for (uint32_t o = 0; o < n16; o += kBinA)
@@ -164,14 +176,14 @@ __global__ __launch_bounds__(256) void k_bin_tag(const double* __restrict__ x, c
     }
 }
 
-template <int D, int T, bool WMSR = false, bool FAULTY = false>
-__global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const double* __restrict__ stage,
+template <int D, int T, bool WMSR = false, bool FAULTY = false, typename VT = double>
+__global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const VT* __restrict__ stage,
                                                        const uint16_t* __restrict__ invpos,
                                                        const uint2* __restrict__ tiles, uint32_t nrun, uint32_t Q,
                                                        uint32_t Qc) {
     static_assert(D % 8 == 0, "invpos is read 8 slots at a time");
-    // runs are padded to even lengths; nrun <= D*kBinSB/16 (checked when the plan is built)
-    __shared__ __attribute__((aligned(16))) double raw[D * kBinSB + D * kBinSB / 16];
+    // runs are padded to 16-byte multiples; nrun <= D*kBinSB/16 (checked when the plan is built)
+    __shared__ __attribute__((aligned(16))) VT raw[D * kBinSB + D * kBinSB / 16 * (16 / sizeof(VT) - 1)];
     InstState* S = a.st;
     if (S->done) return;
     // XCD-aware order: consecutive receiver blocks (which share the lines at their tile-run
@@ -187,7 +199,7 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
     const uint64_t i = a.row0 + li;                              // global receiver
     const bool live = li < a.nrows;
     // ordinary loads first (their wait is the barrier's vmcnt(0) anyway)
-    const double xi = live ? a.xin[i] : 0.0;
+    const VT xi = live ? reinterpret_cast<const VT*>(a.xin)[i] : VT(0);
     uint32_t si = kHonest;
     if constexpr (FAULTY) {
         if (a.status && live) si = a.status[i];
@@ -201,9 +213,9 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
 
     double mn = kInf, mx = -kInf;
     if (live) {
-        double res = xi;
+        VT res = xi;
         if (!FAULTY || is_active(si, a.r)) {
-            double v[D + 1];
+            VT v[D + 1];
             v[0] = xi;
 #pragma unroll
             for (int q = 0; q < D / 8; ++q) {
@@ -242,7 +254,7 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
             }
             res = apply_rule_reg<D, T, WMSR>(a.rule, v);
         }
-        a.xout[i] = res;
+        reinterpret_cast<VT*>(a.xout)[i] = res;
         if (si == kHonest) {
             mn = res;
             mx = res;
@@ -259,6 +271,7 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
 //               bl = (li % SR) / kBinSB                (phase B reads stage2)
 struct BinGeom {
     uint32_t D, dp, SA, P, Q, levels, SR, R, K, PK, QR;
+    uint32_t pad;   // tile lengths padded to 16 bytes: 2 (fp64) or 4 (fp32) elements
 };
 
 __device__ __forceinline__ uint32_t ell_at(const uint32_t* ell, uint64_t i, uint32_t t, uint32_t dp) {
@@ -293,11 +306,12 @@ __global__ __launch_bounds__(256) void k_bin_bounds(uint64_t E, const uint32_t* 
 }
 
 // padded tile lengths (even, so every run starts 16-byte aligned in the stage and in LDS)
-__global__ __launch_bounds__(256) void k_bin_plen(const uint2* __restrict__ tl, uint64_t nt, uint32_t* __restrict__ plen) {
+__global__ __launch_bounds__(256) void k_bin_plen(const uint2* __restrict__ tl, uint64_t nt, uint32_t pad,
+                                                  uint32_t* __restrict__ plen) {
     const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (k >= nt) return;
     const uint2 t = tl[k];
-    plen[k] = t.y ? (t.y - t.x + 1u) & ~1u : 0u;
+    plen[k] = t.y ? (t.y - t.x + pad - 1u) & ~(pad - 1u) : 0u;
 }
 
 // idxA[padded position] = sender index inside its source block (level-1 order)
@@ -499,7 +513,7 @@ hipError_t tile_sort(const uint32_t* ell, uint64_t E, const BinGeom& G, int leve
     if (e == hipSuccess) e = hipcub::DeviceRadixSort::SortPairs(temp, tb, keys, T.ks, vals, T.vs, (int)E, 0, bits, s);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_bin_bounds, dim3(grid), dim3(256), 0, s, E, T.ks, T.tl);
-        hipLaunchKernelGGL(k_bin_plen, dim3(gridt), dim3(256), 0, s, T.tl, nt, T.plen);
+        hipLaunchKernelGGL(k_bin_plen, dim3(gridt), dim3(256), 0, s, T.tl, nt, G.pad, T.plen);
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(temp, tb, T.plen, T.pstart, (int)nt, s);
@@ -518,7 +532,7 @@ hipError_t tile_sort(const uint32_t* ell, uint64_t E, const BinGeom& G, int leve
 }  // namespace
 
 hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t NR, uint32_t d, uint32_t dp,
-                        uint32_t sa, bool tagged, hipStream_t s) {
+                        uint32_t sa, bool tagged, bool f32, hipStream_t s) {
     hipError_t e = hipSuccess;
     uint32_t sr = 0;
     const uint32_t levels = binned_levels(N, NR, d, sa, &sr);
@@ -526,6 +540,8 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     BinGeom G{};
     G.D = d;
     G.dp = dp;
+    G.pad = f32 ? 4u : 2u;
+    if (f32 && levels != 1) return hipErrorNotSupported;   // fp32 plans: one level, clean
     G.SA = sa;
     G.P = (uint32_t)((N + sa - 1) / sa);
     G.Q = (uint32_t)((NR + kBinSB - 1) / kBinSB);
@@ -542,6 +558,7 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     G.K = (G.P + G.PK - 1) / G.PK;
     p.D = d;
     p.SA = sa;
+    p.f32 = f32;
     p.P = G.P;
     p.Q = G.Q;
     p.levels = levels;
@@ -562,7 +579,7 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     p.Ep1 = T1.Ep;
     if (e == hipSuccess) e = hipMalloc(&p.idxA, p.Ep1 * 2);
     if (e == hipSuccess) e = hipMemsetAsync(p.idxA, 0, p.Ep1 * 2, s);
-    if (e == hipSuccess) e = hipMalloc(&p.stage1, p.Ep1 * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc(&p.stage1, p.Ep1 * (f32 ? sizeof(float) : sizeof(double)));
     if (e == hipSuccess) e = hipMalloc(&p.aoff, ((uint64_t)G.P + 1) * sizeof(uint64_t));
     if (e == hipSuccess && tagged) e = hipMalloc(&p.xtag, (N + 2) * sizeof(double));
     if (e == hipSuccess) {
@@ -646,13 +663,39 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
 hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool clean, hipStream_t s) {
     static bool attr = false;   // source blocks above 8192 senders / phase-M images need > 64 KiB of LDS
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_scatter),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_scatter<double>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 16384 * sizeof(double));
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_scatter<float>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 16384 * sizeof(double));
         if (e == hipSuccess)
             e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_regroup),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, kBinMCap * sizeof(double));
         if (e != hipSuccess) return e;
         attr = true;
+    }
+    if (p.f32) {   // fp32 plans: one level, clean configs
+        if (!clean || p.levels != 1) return hipErrorNotSupported;
+        float* st1 = reinterpret_cast<float*>(p.stage1);
+        hipLaunchKernelGGL(k_bin_scatter<float>, dim3(p.P * p.segs), dim3(kBinA), p.SA * sizeof(float), s,
+                           reinterpret_cast<const float*>(a.xin), p.idxA, p.aoff, st1, a.st, a.N, p.SA, p.segs,
+                           p.chunk);
+        const uint32_t nslot = a.nblk > p.Q ? a.nblk : p.Q;
+        const uint32_t Qc = (nslot + 7) / 8;
+        const dim3 grid(8 * Qc);
+#define X(DD, TT)                                                                                        \
+    if (p.D == DD && a.trim == TT) {                                                                     \
+        if (a.rule == 4)                                                                                 \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, true, false, float>), grid, dim3(kBinSB), 0, s, a, st1, \
+                               p.invpos, p.tiles, p.nrun, p.Q, Qc);                                      \
+        else                                                                                             \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, false, false, float>), grid, dim3(kBinSB), 0, s, a, st1, \
+                               p.invpos, p.tiles, p.nrun, p.Q, Qc);                                      \
+        return hipGetLastError();                                                                        \
+    }
+        ACS_BINNED_VARIANTS(X)
+#undef X
+        return hipErrorNotSupported;
     }
     const double* src = a.xin;
     if (!clean && a.status) {
@@ -661,7 +704,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
                            a.N, a.r, a.st);
         src = p.xtag;
     }
-    hipLaunchKernelGGL(k_bin_scatter, dim3(p.P * p.segs), dim3(kBinA), p.SA * sizeof(double), s, src, p.idxA, p.aoff,
+    hipLaunchKernelGGL(k_bin_scatter<double>, dim3(p.P * p.segs), dim3(kBinA), p.SA * sizeof(double), s, src, p.idxA, p.aoff,
                        p.stage1, a.st, a.N, p.SA, p.segs, p.chunk);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -34,6 +34,7 @@ sys.path.insert(0, PKG)
 METRIC = "node-rounds/sec (whole node) + % HBM roofline, trimmed-mean N=1M sparse"
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 BYTES_PER_NODE_ROUND = 400  # 32*4 + 32*8 + 8 + 8
+BYTES_PER_NODE_ROUND_F32 = 264  # SURVEY §8(d) fp32 mode: 32*4 + 32*4 + 4 + 4
 
 
 def parse():
@@ -43,6 +44,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--n-nodes", type=int, default=1 << 20)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--dtype", default="f64", choices=["f64", "f32"],
+                   help="value type; the headline is fp64, fp32 mode (DESIGN.md §9) is reported separately")
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="target CPU work for the bounded cpu_baseline sample")
     p.add_argument("--no-event-timing", action="store_true",
@@ -53,14 +56,14 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(n_nodes: int, seconds: float) -> dict:
+def cpu_baseline(n_nodes: int, seconds: float, dtype: str = "f64") -> dict:
     """Time the oracle (oracle/acs_oracle.c, -O2, OpenMP over receivers) on the host cores."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from acsim import preset
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     threads = max(1, min(threads, 16))
-    cfg = preset("cfg4", n_nodes=n_nodes, max_rounds=10000, omp_threads=threads)
+    cfg = preset("cfg4", n_nodes=n_nodes, max_rounds=10000, omp_threads=threads, dtype=dtype)
     with O.OracleSimulator(cfg, threads=threads) as o:
         t0 = time.perf_counter()
         o.round(1)   # warm-up round (page faults, thread spin-up)
@@ -136,8 +139,9 @@ def main():
 
     value = world * n * a.steps / dt
     avg_launch_s = (k_ms / 1e3 / k_n) if k_n else dt / a.steps
-    achieved = BYTES_PER_NODE_ROUND * n / avg_launch_s / 1e9
-    traffic = load_pmc(kname, n)
+    unit_b = BYTES_PER_NODE_ROUND_F32 if a.dtype == "f32" else BYTES_PER_NODE_ROUND
+    achieved = unit_b * n / avg_launch_s / 1e9
+    traffic = load_pmc(kname, n) if a.dtype == "f64" else None
     out = {
         "metric": METRIC,
         "value": value,
@@ -149,7 +153,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f64",
+        "dtype": a.dtype,
         "data": "synthetic (Philox-seeded x^0 and Feistel graph, SURVEY §A.2/§A.3)",
         "config": {"workload": "cfg4: N=2^20 random 32-regular graph, trimmed mean t=5, no faults, "
                                "no loss, FIXED rounds (SURVEY §A.10)",
@@ -158,12 +162,12 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": kname, "avg_launch_us": avg_launch_s * 1e6,
-                     "bytes_per_node_round": BYTES_PER_NODE_ROUND},
-        "hbm_roofline_pct_wall": 100.0 * BYTES_PER_NODE_ROUND * value / world / 1e9 / HBM_PEAK_GBS,
+                     "bytes_per_node_round": unit_b},
+        "hbm_roofline_pct_wall": 100.0 * unit_b * value / world / 1e9 / HBM_PEAK_GBS,
     }
     sim.close()
     if world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(n, a.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(n, a.cpu_seconds, a.dtype)
     else:
         out["cpu_baseline"] = None
     print(json.dumps(out), flush=True)

@@ -80,3 +80,39 @@ def test_f32_virtual_partitions(oracle_mod, parts):
         p.run()
         assert np.array_equal(ref.rounds(), p.rounds())
         assert np.array_equal(ref.values(0).view(np.uint32), p.values(0).view(np.uint32))
+
+
+@pytest.mark.parametrize("n,d,t,rule,sa", [(8192, 32, 5, "trimmed", 1024), (5000, 16, 5, "midpoint", 512),
+                                           (3001, 8, 2, "wmsr", 256), (1 << 20, 32, 5, "trimmed", 16384)])
+def test_f32_binned_matches_per_lane(oracle_mod, n, d, t, rule, sa):
+    """The fp32 binned exchange (float stage, runs padded to 16 B) against the fp32 per-lane kernel
+    and, at oracle-friendly sizes, the oracle."""
+    import os
+    cfg = Config(n_nodes=n, topology="regular", degree=d, rule=rule, trim=t, eps=1e-6,
+                 max_rounds=8 if n > 100000 else 300, termination="fixed" if n > 100000 else "eps",
+                 seed=4, dtype="f32")
+    old = {k: os.environ.get(k) for k in ("ACSIM_BIN_SA", "ACSIM_BINNED")}
+    try:
+        os.environ["ACSIM_BIN_SA"] = str(sa)
+        with acsim.Simulator(cfg, device=0) as g:
+            assert "k_bin_gather" in g.kernel_name() and "f32" in g.kernel_name(), g.kernel_name()
+            g.run()
+            xb, rb = g.values(0), g.rounds()
+        os.environ["ACSIM_BINNED"] = "0"
+        with acsim.Simulator(cfg, device=0) as g:
+            assert "k_round_regular" in g.kernel_name()
+            g.run()
+            xl, rl = g.values(0), g.rounds()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert np.array_equal(rb, rl)
+    assert np.array_equal(xb.view(np.uint32), xl.view(np.uint32))
+    if n <= 10000:
+        with oracle_mod.OracleSimulator(cfg, threads=8) as o:
+            o.run()
+            assert np.array_equal(o.rounds(), rb)
+            assert np.array_equal(o.values(0).view(np.uint32), xb.view(np.uint32))

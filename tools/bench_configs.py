@@ -23,11 +23,15 @@ CASES = {
     "cfg4_eps": dict(),
     "cfg4_byz": dict(),
     "cfg5": dict(max_rounds=20),
+    "cfg4_f32": dict(max_rounds=100),   # fp32 mode
 }
 
 
 def run(name, **kw):
-    cfg = acsim.preset(name, **kw)
+    if name.endswith("_f32"):
+        cfg = acsim.preset(name[:-4], dtype="f32", **kw)
+    else:
+        cfg = acsim.preset(name, **kw)
     t0 = time.perf_counter()
     sim = acsim.Simulator(cfg)
     t_setup = time.perf_counter() - t0
