@@ -68,7 +68,7 @@ def cpu_baseline(n_nodes: int, seconds: float, dtype: str = "f64") -> dict:
         t0 = time.perf_counter()
         o.round(1)   # warm-up round (page faults, thread spin-up)
         one = time.perf_counter() - t0
-        rounds = int(max(1, min(50, seconds / max(one, 1e-3))))
+        rounds = int(max(1, min(1000, seconds / max(one, 1e-3))))
         t0 = time.perf_counter()
         o.round(rounds)
         dt = time.perf_counter() - t0
@@ -78,9 +78,9 @@ def cpu_baseline(n_nodes: int, seconds: float, dtype: str = "f64") -> dict:
                       f"round, {dt:.1f} s, oracle/acs_oracle.c with {threads} OpenMP threads"}
 
 
-def load_pmc(kernel: str, n_nodes: int):
+def load_pmc(kernel: str, n_nodes: int, dtype: str = "f64"):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if one matches."""
-    path = os.path.join(ROOT, "profiles", "pmc_cfg4.json")
+    path = os.path.join(ROOT, "profiles", "pmc_cfg4.json" if dtype == "f64" else "pmc_cfg4_f32.json")
     try:
         d = json.load(open(path))
     except Exception:
@@ -103,7 +103,8 @@ def main():
     import acsim
 
     n = a.n_nodes
-    cfg = acsim.preset("cfg4", n_nodes=n, max_rounds=a.warmup + a.steps, instance_offset=rank)
+    cfg = acsim.preset("cfg4", n_nodes=n, max_rounds=a.warmup + a.steps, instance_offset=rank,
+                         dtype=a.dtype)
     sim = acsim.Simulator(cfg, device=local_rank if world > 1 else 0)
 
     def barrier_sync():
@@ -141,7 +142,7 @@ def main():
     avg_launch_s = (k_ms / 1e3 / k_n) if k_n else dt / a.steps
     unit_b = BYTES_PER_NODE_ROUND_F32 if a.dtype == "f32" else BYTES_PER_NODE_ROUND
     achieved = unit_b * n / avg_launch_s / 1e9
-    traffic = load_pmc(kname, n) if a.dtype == "f64" else None
+    traffic = load_pmc(kname, n, a.dtype)
     out = {
         "metric": METRIC,
         "value": value,
