@@ -69,7 +69,7 @@ extern "C" {
 #define ACS_TERM_EPS    0
 #define ACS_TERM_FIXED  1
 
-/* value type (§A.0).  Only ACS_F64 is implemented in this round. */
+/* value type (§A.0): fp64, or binary32 throughout */
 #define ACS_F64 0
 #define ACS_F32 1
 
@@ -106,7 +106,7 @@ typedef struct acs_config {
     double   eps;              /* ε */
     uint32_t max_rounds;       /* round cap (EPS) or exact round count (FIXED) */
     uint32_t termination;      /* ACS_TERM_* */
-    uint32_t dtype;            /* ACS_F64 */
+    uint32_t dtype;            /* ACS_F64 | ACS_F32 */
     uint64_t seed;             /* Philox key for every stream except GRAPH */
     uint64_t graph_seed;       /* Philox key for GRAPH; 0 means "use seed" */
     uint32_t trace_spread;     /* 1: keep spread^r for every round (per instance) */
