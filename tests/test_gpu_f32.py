@@ -116,3 +116,34 @@ def test_f32_binned_matches_per_lane(oracle_mod, n, d, t, rule, sa):
             o.run()
             assert np.array_equal(o.rounds(), rb)
             assert np.array_equal(o.values(0).view(np.uint32), xb.view(np.uint32))
+
+
+def test_f32_rccl_single_rank_path():
+    """fp32 node partition with a real RCCL communicator (1 rank): ncclFloat32 all-gather."""
+    import ctypes as C
+    lib = acsim._abi.load_library()
+    n = lib.acs_comm_id_size()
+    buf = C.create_string_buffer(n)
+    acsim._abi.check(lib, lib.acs_get_comm_id(buf, n))
+    cfg = preset("cfg5", n_nodes=1 << 17, max_rounds=10, trace_spread=True, dtype="f32")
+    with acsim.Simulator(cfg) as ref, acsim.Simulator(cfg, partitions=1, rank=0, comm_id=buf.raw) as p:
+        ref.run()
+        p.run()
+        assert np.array_equal(p.rounds(), ref.rounds())
+        assert np.array_equal(p.values(0).view(np.uint32), ref.values(0).view(np.uint32))
+        assert np.array_equal(p.spread_trace(0), ref.spread_trace(0))
+
+
+def test_f32_csr_matches_oracle(oracle_mod):
+    from test_csr import random_csr
+    rowptr, colidx = random_csr(500, 6, 20, 1)
+    cfg = Config(n_nodes=500, topology="csr", rule="trimmed", trim=2, fault_model="byzantine", n_faulty=20,
+                 byz_strategy="random", byz_delta=0.1, loss_p=0.05, eps=1e-6, seed=4, max_rounds=300,
+                 trace_spread=True, dtype="f32")
+    with acsim.Simulator(cfg, device=0, csr=(rowptr, colidx)) as g, \
+            oracle_mod.OracleSimulator(cfg, csr=(rowptr, colidx)) as o:
+        g.run()
+        o.run()
+        assert np.array_equal(g.rounds(), o.rounds())
+        assert np.array_equal(g.values(0).view(np.uint32), o.values(0).view(np.uint32))
+        assert np.array_equal(g.spread_trace(0), o.spread_trace(0))
