@@ -116,7 +116,12 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
     extern __shared__ __attribute__((aligned(16))) unsigned char lx_raw[];
     VT* lx = reinterpret_cast<VT*>(lx_raw);
     if (st->done) return;
-    const uint32_t a = blockIdx.x / segs, sg = blockIdx.x % segs;
+    // XCD-aware order (dispatch deals blocks round-robin over the 8 XCDs): every segment of source
+    // block a runs on the XCD of blockIdx % 8 = a % 8, so its x block is fetched into one L2 once
+    // instead of once per XCD.  The grid is 8 * ceil(P / 8) * segs.
+    const uint32_t slot = blockIdx.x >> 3;
+    const uint32_t a = (slot / segs) * 8 + (blockIdx.x & 7u), sg = slot % segs;
+    if ((uint64_t)a * SA >= N) return;   // padding past the last source block
     const uint64_t pa1 = aoff[a + 1];
     const uint64_t p0 = aoff[a] + (uint64_t)sg * chunk;
     if (p0 >= pa1) return;
@@ -677,7 +682,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
     if (p.f32) {   // fp32 plans: one level, clean configs
         if (!clean || p.levels != 1) return hipErrorNotSupported;
         float* st1 = reinterpret_cast<float*>(p.stage1);
-        hipLaunchKernelGGL(k_bin_scatter<float>, dim3(p.P * p.segs), dim3(kBinA), p.SA * sizeof(float), s,
+        hipLaunchKernelGGL(k_bin_scatter<float>, dim3((p.P + 7) / 8 * 8 * p.segs), dim3(kBinA), p.SA * sizeof(float), s,
                            reinterpret_cast<const float*>(a.xin), p.idxA, p.aoff, st1, a.st, a.N, p.SA, p.segs,
                            p.chunk);
         const uint32_t nslot = a.nblk > p.Q ? a.nblk : p.Q;
@@ -704,7 +709,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
                            a.N, a.r, a.st);
         src = p.xtag;
     }
-    hipLaunchKernelGGL(k_bin_scatter<double>, dim3(p.P * p.segs), dim3(kBinA), p.SA * sizeof(double), s, src, p.idxA, p.aoff,
+    hipLaunchKernelGGL(k_bin_scatter<double>, dim3((p.P + 7) / 8 * 8 * p.segs), dim3(kBinA), p.SA * sizeof(double), s, src, p.idxA, p.aoff,
                        p.stage1, a.st, a.N, p.SA, p.segs, p.chunk);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
