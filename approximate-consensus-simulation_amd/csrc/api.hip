@@ -653,6 +653,11 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     uint32_t bin_sa = sa_max;
     if (const char* v = getenv("ACSIM_BIN_SA")) bin_sa = (uint32_t)strtoul(v, nullptr, 10);
     if (bin_sa < 64 || bin_sa > sa_max || (bin_sa & (bin_sa - 1))) bin_sa = sa_max;
+    // order-free phase B (clean, sort-based rule: the rows are stored sorted and the rule sees a
+    // multiset), ACSIM_BIN_OF=1: measured slower than the invpos phase B, kept as
+    // a tested variant
+    const char* of_env = getenv("ACSIM_BIN_OF");
+    const bool bin_of = s->ell_sorted && of_env && of_env[0] == '1';
     {
         const char* env = getenv("ACSIM_BINNED");
         const bool allow = !(env && env[0] == '0');
@@ -721,7 +726,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         CREATE_TRY(build_rows(s, s->ell, partitioned ? rank : 0));
         if (s->binned) {   // the plan replaces the ELL in the round loop
             const uint64_t nr = partitioned ? part_rows(s, rank) : s->N;
-            if (nr) CREATE_TRY(binned_build(s->bin, s->ell, s->N, nr, s->d, s->dp, bin_sa, tagged, s->f32, s->stream));
+            if (nr) CREATE_TRY(binned_build(s->bin, s->ell, s->N, nr, s->d, s->dp, bin_sa, tagged, s->f32, bin_of, s->stream));
             (void)hipFree(s->ell);
             s->ell = nullptr;
         }
@@ -736,7 +741,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
                 CREATE_TRY(build_rows(s, q.ell, p));
                 if (s->binned) {
                     const uint64_t nr = part_rows(s, p);
-                    if (nr) CREATE_TRY(binned_build(q.bin, q.ell, s->N, nr, s->d, s->dp, bin_sa, tagged, s->f32, s->stream));
+                    if (nr) CREATE_TRY(binned_build(q.bin, q.ell, s->N, nr, s->d, s->dp, bin_sa, tagged, s->f32, bin_of, s->stream));
                     (void)hipFree(q.ell);
                     q.ell = nullptr;
                 }

@@ -123,7 +123,10 @@ struct BinnedPlan {
     uint16_t* idxA = nullptr;           // [Ep1] sender index within its source block (0 in pads)
     uint16_t* idxM = nullptr;           // [Ep2] position inside the phase-M LDS image (two levels)
     uint16_t* invpos = nullptr;         // [Q][D/8][kBinSB][8]: position of (receiver, slot) in block b's runs
-    uint2* tiles = nullptr;             // [Q][nrun+1] (stage start, element offset in block b's runs)
+    uint2* tiles = nullptr;             // [Q][nrun+1] (stage start | pad count, element offset in block b's runs)
+    bool ofree = false;                 // order-free phase B (rid, no invpos)
+    uint32_t rstride = 0;               // bytes per receiver block in rid
+    uint8_t* rid = nullptr;             // [Q][rstride] receiver inside block b of each image position (ofree)
     uint2* mt = nullptr;                // [ngroups][PK+1] phase-M run tables (two levels)
     uint64_t* aoff = nullptr;           // [P+1] stage1 start of source block a
     uint64_t* moff = nullptr;           // [ngroups+1] stage2 start of phase-M group g
@@ -135,9 +138,10 @@ bool binned_supported(uint32_t d, uint32_t t, uint32_t rule);
 // 1 or 2 exchange levels for NR local receivers of an N-node graph (0: not supported).
 uint32_t binned_levels(uint64_t N, uint64_t NR, uint32_t d, uint32_t sa, uint32_t* sr_out);
 // Builds the plan from the ELL of the NR local rows (sorted or spec order; slot-dependent configs
-// need spec order); sa = source block size; tagged: the config has a fault schedule.
+// need spec order); sa = source block size; tagged: the config has a fault schedule; ofree: clean
+// config under a sort-based rule (order-free phase B: rid instead of invpos).
 hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t NR, uint32_t d, uint32_t dp,
-                        uint32_t sa, bool tagged, bool f32, hipStream_t s);
+                        uint32_t sa, bool tagged, bool f32, bool ofree, hipStream_t s);
 void binned_free(BinnedPlan& p);
 // clean: no slot-dependent decision (selects the plain phase-B instantiation)
 hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool clean, hipStream_t s);

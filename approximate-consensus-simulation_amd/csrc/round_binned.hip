@@ -42,6 +42,11 @@ namespace acs {
 
 constexpr uint32_t kBinA = 512;        // phase-A / phase-M workgroup: 8 waves
 constexpr uint32_t kBinMCap = 19456;   // phase-M LDS image capacity (elements, 152 KiB)
+// cache-policy switches of the exchange (launch argument `pol`; ACSIM_BIN_POL overrides the default)
+constexpr uint32_t kPolNtRuns = 1;     // phase B: stage runs by nontemporal LDS-DMA
+constexpr uint32_t kPolNtStore = 2;    // phase A / M: nontemporal stage stores
+constexpr uint32_t kPolNtInv = 4;      // phase B: nontemporal invpos loads
+constexpr uint32_t kPolDefault = kPolNtStore | kPolNtInv;   // measured: phase B 80 -> 71 us, phase A -1 us (cfg4)
 
 // ------------------------------------------------------------------------------ shared pieces
 // Stream [p0, p1) of an index stream: out[p] = lds[idx[p]].  Super-steps of 512 positions per
@@ -53,7 +58,7 @@ __device__ __forceinline__ float2 bin_pair(float a, float b) { return make_float
 // VT = double, or float for fp32 plans (the instruction's store is then 8 bytes)
 template <typename VT = double>
 __device__ __forceinline__ void bin_stream(const VT* lx, const uint16_t* __restrict__ idx, VT* __restrict__ out,
-                                           uint64_t p0, uint64_t p1) {
+                                           uint64_t p0, uint64_t p1, bool nt_store = false) {
     using V2 = decltype(bin_pair(VT(0), VT(0)));
     constexpr uint32_t SUP = kBinA / 64 * 512, SUPW = SUP / 2;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -68,7 +73,16 @@ __device__ __forceinline__ void bin_stream(const VT* lx, const uint16_t* __restr
 #pragma unroll
             for (int q = 0; q < 4; ++q) c[q] = __builtin_nontemporal_load(ip + k * SUPW + q * 64);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) op[k * SUPW + q * 64] = bin_pair(lx[c[q] & 0xFFFFu], lx[c[q] >> 16]);
+            for (int q = 0; q < 4; ++q) {
+                const V2 v = bin_pair(lx[c[q] & 0xFFFFu], lx[c[q] >> 16]);
+                if (nt_store) {   // as an integer vector of V2's size (the builtin takes native vector types)
+                    using UV = unsigned int __attribute__((ext_vector_type(sizeof(V2) / 4)));
+                    UV bits;
+                    __builtin_memcpy(&bits, &v, sizeof(V2));
+                    __builtin_nontemporal_store(bits, reinterpret_cast<UV*>(op + k * SUPW + q * 64));
+                } else
+                    op[k * SUPW + q * 64] = v;
+            }
         }
         p = p0 + nsup * SUP;
     }
@@ -82,7 +96,7 @@ __device__ __forceinline__ void bin_stream(const VT* lx, const uint16_t* __restr
 // Runs are padded to EPU = 16 / sizeof(VT) elements (2 for fp64, 4 for fp32).
 template <typename VT = double>
 __device__ __forceinline__ void bin_dma_runs(const uint2* __restrict__ tb, uint32_t r0, uint32_t r1,
-                                             const VT* __restrict__ src, VT* dst) {
+                                             const VT* __restrict__ src, VT* dst, bool nt = false) {
     constexpr uint32_t EPU = 16 / sizeof(VT);
     const uint32_t lane = threadIdx.x & 63;
     const uint4* s16 = reinterpret_cast<const uint4*>(src);
@@ -101,8 +115,13 @@ __device__ __forceinline__ void bin_dma_runs(const uint2* __restrict__ tb, uint3
             const uint32_t n16 = (__builtin_amdgcn_readlane(nxt, k) - pre) / EPU;   // 16-byte units
             const uint4* sp = s16 + so / EPU + lane;
             uint4* dp = d16 + pre / EPU;
-            for (uint32_t o = 0; o < n16; o += 64)
-                if (o + lane < n16) __builtin_amdgcn_global_load_lds(sp + o, dp + o, 16, 0, 0);
+            if (nt) {   // once-read runs: nontemporal policy (aux = 2)
+                for (uint32_t o = 0; o < n16; o += 64)
+                    if (o + lane < n16) __builtin_amdgcn_global_load_lds(sp + o, dp + o, 16, 0, 2);
+            } else {
+                for (uint32_t o = 0; o < n16; o += 64)
+                    if (o + lane < n16) __builtin_amdgcn_global_load_lds(sp + o, dp + o, 16, 0, 0);
+            }
         }
     }
 }
@@ -112,7 +131,7 @@ template <typename VT = double>
 __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x, const uint16_t* __restrict__ idxA,
                                                      const uint64_t* __restrict__ aoff, VT* __restrict__ stage,
                                                      const InstState* __restrict__ st, uint64_t N, uint32_t SA,
-                                                     uint32_t segs, uint32_t chunk) {
+                                                     uint32_t segs, uint32_t chunk, uint32_t pol) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lx_raw[];
     VT* lx = reinterpret_cast<VT*>(lx_raw);
     if (st->done) return;
@@ -138,7 +157,7 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
             if (o + threadIdx.x < n16) __builtin_amdgcn_global_load_lds(xs + o, ld + o, 16, 0, 0);
     }
     __syncthreads();
-    bin_stream(lx, idxA, stage, p0, p1);
+    bin_stream(lx, idxA, stage, p0, p1, (pol & kPolNtStore) != 0);
 }
 
 // ------------------------------------------------------------------------------ phase M
@@ -185,7 +204,7 @@ template <int D, int T, bool WMSR = false, bool FAULTY = false, typename VT = do
 __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const VT* __restrict__ stage,
                                                        const uint16_t* __restrict__ invpos,
                                                        const uint2* __restrict__ tiles, uint32_t nrun, uint32_t Q,
-                                                       uint32_t Qc) {
+                                                       uint32_t Qc, uint32_t pol) {
     static_assert(D % 8 == 0, "invpos is read 8 slots at a time");
     // runs are padded to 16-byte multiples; nrun <= D*kBinSB/16 (checked when the plan is built)
     __shared__ __attribute__((aligned(16))) VT raw[D * kBinSB + D * kBinSB / 16 * (16 / sizeof(VT) - 1)];
@@ -211,9 +230,20 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
     }
     uint4 ip[D / 8];
     const uint4* ipp = reinterpret_cast<const uint4*>(invpos) + (uint64_t)b * (D / 8) * kBinSB + threadIdx.x;
+    if (pol & kPolNtInv) {
+        using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+        const u32x4* ipn = reinterpret_cast<const u32x4*>(ipp);
 #pragma unroll
-    for (int q = 0; q < D / 8; ++q) ip[q] = ipp[q * kBinSB];
-    bin_dma_runs(tiles + (uint64_t)b * (nrun + 1), w * nrun / NW, (w + 1) * nrun / NW, stage, raw);
+        for (int q = 0; q < D / 8; ++q) {
+            const u32x4 t4 = __builtin_nontemporal_load(ipn + q * kBinSB);
+            ip[q] = make_uint4(t4.x, t4.y, t4.z, t4.w);
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < D / 8; ++q) ip[q] = ipp[q * kBinSB];
+    }
+    bin_dma_runs(tiles + (uint64_t)b * (nrun + 1), w * nrun / NW, (w + 1) * nrun / NW, stage, raw,
+                 (pol & kPolNtRuns) != 0);
     __syncthreads();
 
     double mn = kInf, mx = -kInf;
@@ -264,6 +294,163 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
             mn = res;
             mx = res;
         }
+    }
+    block_minmax_store<kBinSB>(mn, mx, a.partial + b);
+}
+
+// ------------------------------------------------------------------------------ phase B, order-free
+// Clean configs under the sort-based rules (TRIMMED / MIDPOINT / DLPSW / W-MSR) hand the rule a
+// multiset: the slot order of a receiver's values is free.  Phase B then needs no (receiver, slot)
+// position table.  rid[b][image position] (u8: 1 B per delivery instead of invpos's 2 B) names the
+// receiver of each entry of block b's concatenated runs; the runs are loaded into registers (16 B
+// per lane, up to RB runs per wave in flight together), and a per-receiver LDS counter hands out
+// slots in dst[slot][receiver].  The slot an entry lands in may differ between launches; every
+// receiver's multiset, and so the rule's result, does not.  Run padding is excluded through the
+// pad count kept in the low bits of each run's (16-byte aligned) stage start.
+template <int D, int T, bool WMSR = false, typename VT = double>
+__global__ __launch_bounds__(kBinSB) void k_bin_gather_of(const RoundArgs a, const VT* __restrict__ stage,
+                                                          const uint8_t* __restrict__ rid, uint32_t rstride,
+                                                          const uint2* __restrict__ tiles, uint32_t nrun, uint32_t Q,
+                                                          uint32_t Qc) {
+    constexpr uint32_t EPU = 16 / sizeof(VT);
+    constexpr uint32_t RB = 16;
+    constexpr uint32_t NW = kBinSB / 64;
+    constexpr uint32_t kRidCap = D * kBinSB + D * kBinSB / 16 * (EPU - 1);
+    __shared__ __attribute__((aligned(16))) VT dst[D * kBinSB + 64];         // + one dummy slot per lane
+    __shared__ __attribute__((aligned(16))) uint8_t lrid[kRidCap + 16];
+    __shared__ uint32_t cnt[kBinSB + 64];                                      // + one dummy counter per lane
+    InstState* S = a.st;
+    if (S->done) return;
+    const uint32_t b = (blockIdx.x & 7u) * Qc + (blockIdx.x >> 3);   // XCD-aware, as k_bin_gather
+    if (b >= Q) {
+        if (b < a.nblk && threadIdx.x == 0) a.partial[b] = make_double2(kInf, -kInf);
+        return;
+    }
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t li = (uint64_t)b * kBinSB + threadIdx.x;
+    const uint64_t i = a.row0 + li;
+    const bool live = li < a.nrows;
+    const VT xi = live ? reinterpret_cast<const VT*>(a.xin)[i] : VT(0);
+    cnt[threadIdx.x] = 0;
+    if (threadIdx.x < 64) cnt[kBinSB + threadIdx.x] = 0;
+    {   // block b's rid image -> LDS (rstride is a multiple of 16 and fits lrid)
+        const uint32_t n16 = rstride / 16;
+        const uint4* src = reinterpret_cast<const uint4*>(rid + (uint64_t)b * rstride) + threadIdx.x;
+        uint4* ld = reinterpret_cast<uint4*>(lrid) + (threadIdx.x & ~63u);
+        for (uint32_t o = 0; o < n16; o += kBinSB)
+            if (o + threadIdx.x < n16) __builtin_amdgcn_global_load_lds(src + o, ld + o, 16, 0, 0);
+    }
+    const uint2* tb = tiles + (uint64_t)b * (nrun + 1);
+    const uint4* s16 = reinterpret_cast<const uint4*>(stage);
+    const uint32_t r0 = w * nrun / NW, r1 = (w + 1) * nrun / NW;
+    const uint32_t nb = ((nrun + NW - 1) / NW + RB - 1) / RB;   // the same batch count in every wave
+    for (uint32_t it = 0; it < nb; ++it) {
+        const uint32_t g = r0 + it * RB;
+        const uint32_t ng = g < r1 ? (r1 - g < RB ? r1 - g : RB) : 0u;
+        uint32_t so_l = 0, pre_l = 0, nxt_l = 0;
+        if (lane < ng) {
+            const uint2 dd = tb[g + lane];
+            so_l = dd.x;
+            pre_l = dd.y;
+            nxt_l = tb[g + lane + 1].y;
+        }
+        // Loads with no control flow around them (a branch here makes the wait-count pass wait for
+        // every load in flight at the join): lanes past a run's end, and runs past ng (zero
+        // descriptors), re-read a valid address instead.
+        uint4 v0[RB], v1[RB];
+#pragma unroll
+        for (uint32_t k = 0; k < RB; ++k) {
+            const uint32_t so = __builtin_amdgcn_readlane(so_l, k), pre = __builtin_amdgcn_readlane(pre_l, k);
+            const uint32_t n16 = (__builtin_amdgcn_readlane(nxt_l, k) - pre) / EPU;
+            const uint4* sp = n16 ? s16 + so / EPU : s16;
+            v0[k] = sp[lane < n16 ? lane : 0u];
+            v1[k] = sp[64 + lane < n16 ? 64 + lane : 0u];
+        }
+        if (it == 0) __syncthreads();   // rid image and counters in place
+        // Consume in groups of 4 runs, each step issued for the whole group before the next (no
+        // branch in between): receiver ids from LDS, the slot atomics, the value writes.  Entries
+        // past a run's end (padding, idle lanes) go to a per-lane dummy counter and dummy slot.
+        using RT = typename std::conditional<EPU == 2, uint16_t, uint32_t>::type;   // EPU ids per read
+#pragma unroll
+        for (uint32_t k0 = 0; k0 < RB; k0 += 4) {
+            uint32_t rr[4][2][EPU];
+            VT vv[4][2][EPU];
+#pragma unroll
+            for (uint32_t k = k0; k < k0 + 4; ++k) {
+                const uint32_t so = __builtin_amdgcn_readlane(so_l, k), pre = __builtin_amdgcn_readlane(pre_l, k);
+                const uint32_t len = __builtin_amdgcn_readlane(nxt_l, k) - pre;
+                const uint32_t nreal = len - (so & (EPU - 1));   // 0 past ng
+#pragma unroll
+                for (uint32_t u = 0; u < 2; ++u) {
+                    const uint32_t e = (u * 64 + lane) * EPU;
+                    uint32_t pos = pre + e;
+                    pos = pos < kRidCap ? pos : 0u;
+                    const uint32_t ids = *reinterpret_cast<const RT*>(lrid + pos);
+                    __builtin_memcpy(vv[k - k0][u], u ? &v1[k] : &v0[k], 16);
+#pragma unroll
+                    for (uint32_t q = 0; q < EPU; ++q)
+                        rr[k - k0][u][q] = e + q < nreal ? (ids >> (8 * q)) & 0xFFu : kBinSB + lane;
+                }
+            }
+            uint32_t sl[4][2][EPU];
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k)
+#pragma unroll
+                for (uint32_t u = 0; u < 2; ++u)
+#pragma unroll
+                    for (uint32_t q = 0; q < EPU; ++q)
+                        sl[k][u][q] = __hip_atomic_fetch_add(&cnt[rr[k][u][q]], 1u, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k)
+#pragma unroll
+                for (uint32_t u = 0; u < 2; ++u)
+#pragma unroll
+                    for (uint32_t q = 0; q < EPU; ++q) {
+                        const uint32_t r = rr[k][u][q];
+                        const uint32_t s2 = sl[k][u][q] < (uint32_t)D ? sl[k][u][q] : (uint32_t)D - 1;
+                        dst[r < kBinSB ? s2 * kBinSB + r : D * kBinSB + lane] = vv[k][u][q];
+                    }
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < RB; ++k) {   // runs longer than 128 units (rare)
+            if (k < ng) {
+                const uint32_t so = __builtin_amdgcn_readlane(so_l, k), pre = __builtin_amdgcn_readlane(pre_l, k);
+                const uint32_t len = __builtin_amdgcn_readlane(nxt_l, k) - pre;
+                const uint32_t n16 = len / EPU, nreal = len - (so & (EPU - 1));
+                const uint4* sp = s16 + so / EPU;
+                for (uint32_t o = 128; o < n16; o += 64) {
+                    if (o + lane < n16) {
+                        const uint4 u4 = sp[o + lane];
+                        VT val[EPU];
+                        __builtin_memcpy(val, &u4, 16);
+#pragma unroll
+                        for (uint32_t q = 0; q < EPU; ++q) {
+                            const uint32_t e = (o + lane) * EPU + q;
+                            if (e < nreal) {
+                                const uint32_t r = lrid[pre + e];
+                                const uint32_t s2 = atomicAdd(&cnt[r], 1u);
+                                dst[(s2 < (uint32_t)D ? s2 : (uint32_t)D - 1) * kBinSB + r] = val[q];
+                            }
+                        }
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    double mn = kInf, mx = -kInf;
+    if (live) {
+        VT v[D + 1];
+        v[0] = xi;
+#pragma unroll
+        for (int t = 0; t < D; ++t) v[1 + t] = dst[t * kBinSB + threadIdx.x];
+        const VT res = apply_rule_reg<D, T, WMSR>(a.rule, v);
+        reinterpret_cast<VT*>(a.xout)[i] = res;
+        mn = res;
+        mx = res;
     }
     block_minmax_store<kBinSB>(mn, mx, a.partial + b);
 }
@@ -397,15 +584,19 @@ __device__ __forceinline__ uint64_t bin_run_key(const BinGeom& G, uint32_t b, ui
     return ((uint64_t)(b / G.QR) * G.K + j) * G.QR + b % G.QR;
 }
 
-// tiles[b][j] = (padded start, element offset inside block b's concatenated runs); tiles[b][nrun] = (0, total)
+// tiles[b][j] = (padded start | pad count, element offset inside block b's concatenated runs);
+// tiles[b][nrun] = (0, total).  Starts are multiples of the pad unit, so the low bits carry the
+// number of padding entries at the run's end (read by the order-free phase B).
 __global__ __launch_bounds__(256) void k_bin_prefix(const uint32_t* __restrict__ pstart, const uint32_t* __restrict__ plen,
-                                                    BinGeom G, uint32_t nrun, uint2* __restrict__ tiles) {
+                                                    const uint2* __restrict__ tl, BinGeom G, uint32_t nrun,
+                                                    uint2* __restrict__ tiles) {
     const uint32_t b = blockIdx.x * 256 + threadIdx.x;
     if (b >= G.Q) return;
     uint32_t pre = 0;
     for (uint32_t j = 0; j < nrun; ++j) {
         const uint64_t key = bin_run_key(G, b, j);
-        tiles[(uint64_t)b * (nrun + 1) + j] = make_uint2(pstart[key], pre);
+        const uint32_t npad = plen[key] - (tl[key].y - tl[key].x);
+        tiles[(uint64_t)b * (nrun + 1) + j] = make_uint2(pstart[key] | npad, pre);
         pre += plen[key];
     }
     tiles[(uint64_t)b * (nrun + 1) + nrun] = make_uint2(0u, pre);
@@ -424,6 +615,21 @@ __global__ __launch_bounds__(256) void k_bin_inv(uint64_t E, BinGeom G, uint32_t
     const uint32_t j = G.levels == 1 ? key / G.Q : (key / G.QR) % G.K;
     const uint32_t pos = tiles[(uint64_t)b * (nrun + 1) + j].y + (uint32_t)(p - tl[key].x);
     invpos[(((uint64_t)b * (G.D / 8) + t / 8) * kBinSB + (li % kBinSB)) * 8 + (t & 7)] = (uint16_t)pos;
+}
+
+// rid[b][pos] = receiver (inside block b) of the entry at image position pos (order-free plans)
+__global__ __launch_bounds__(256) void k_bin_rid(uint64_t E, BinGeom G, uint32_t nrun, uint32_t rstride,
+                                                 const uint32_t* __restrict__ ks, const uint32_t* __restrict__ vs,
+                                                 const uint2* __restrict__ tl, const uint2* __restrict__ tiles,
+                                                 uint8_t* __restrict__ rid) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= E) return;
+    const uint32_t e = vs[p], key = ks[p];
+    const uint64_t li = e / G.D;
+    const uint32_t b = (uint32_t)(li / kBinSB);
+    const uint32_t j = G.levels == 1 ? key / G.Q : (key / G.QR) % G.K;
+    const uint32_t pos = tiles[(uint64_t)b * (nrun + 1) + j].y + (uint32_t)(p - tl[key].x);
+    rid[(uint64_t)b * rstride + pos] = (uint8_t)(li % kBinSB);
 }
 
 // ------------------------------------------------------------------------------ host side
@@ -460,6 +666,7 @@ void binned_free(BinnedPlan& p) {
     (void)hipFree(p.idxA);
     (void)hipFree(p.idxM);
     (void)hipFree(p.invpos);
+    (void)hipFree(p.rid);
     (void)hipFree(p.tiles);
     (void)hipFree(p.mt);
     (void)hipFree(p.aoff);
@@ -537,7 +744,7 @@ hipError_t tile_sort(const uint32_t* ell, uint64_t E, const BinGeom& G, int leve
 }  // namespace
 
 hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t NR, uint32_t d, uint32_t dp,
-                        uint32_t sa, bool tagged, bool f32, hipStream_t s) {
+                        uint32_t sa, bool tagged, bool f32, bool ofree, hipStream_t s) {
     hipError_t e = hipSuccess;
     uint32_t sr = 0;
     const uint32_t levels = binned_levels(N, NR, d, sa, &sr);
@@ -634,15 +841,30 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     }
     // ---- phase B tables over the last stage
     const uint64_t Qp = (uint64_t)G.Q * kBinSB;   // receiver slots incl. the ragged last block's padding
-    if (e == hipSuccess) e = hipMalloc(&p.invpos, Qp * d * 2);
-    if (e == hipSuccess) e = hipMemsetAsync(p.invpos, 0, Qp * d * 2, s);
     if (e == hipSuccess) e = hipMalloc(&p.tiles, ((uint64_t)p.nrun + 1) * G.Q * sizeof(uint2));
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_bin_prefix, dim3((G.Q + 255) / 256), dim3(256), 0, s, last->pstart, last->plen, G, p.nrun,
-                           p.tiles);
-        hipLaunchKernelGGL(k_bin_inv, dim3(grid), dim3(256), 0, s, E, G, p.nrun, last->ks, last->vs, last->tl, p.tiles,
-                           p.invpos);
+        hipLaunchKernelGGL(k_bin_prefix, dim3((G.Q + 255) / 256), dim3(256), 0, s, last->pstart, last->plen, last->tl, G,
+                           p.nrun, p.tiles);
         e = hipGetLastError();
+    }
+    p.ofree = ofree;
+    if (ofree) {   // order-free phase B: receiver ids in image order
+        p.rstride = ((uint32_t)d * kBinSB + p.nrun * (G.pad - 1) + 15u) & ~15u;
+        if (e == hipSuccess) e = hipMalloc(&p.rid, (uint64_t)G.Q * p.rstride);
+        if (e == hipSuccess) e = hipMemsetAsync(p.rid, 0, (uint64_t)G.Q * p.rstride, s);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_bin_rid, dim3(grid), dim3(256), 0, s, E, G, p.nrun, p.rstride, last->ks, last->vs,
+                               last->tl, p.tiles, p.rid);
+            e = hipGetLastError();
+        }
+    } else {
+        if (e == hipSuccess) e = hipMalloc(&p.invpos, Qp * d * 2);
+        if (e == hipSuccess) e = hipMemsetAsync(p.invpos, 0, Qp * d * 2, s);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_bin_inv, dim3(grid), dim3(256), 0, s, E, G, p.nrun, last->ks, last->vs, last->tl,
+                               p.tiles, p.invpos);
+            e = hipGetLastError();
+        }
     }
     hipError_t e2 = hipStreamSynchronize(s);
     if (e == hipSuccess) e = e2;
@@ -666,6 +888,10 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
 }
 
 hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool clean, hipStream_t s) {
+    static const uint32_t pol = [] {
+        const char* v = getenv("ACSIM_BIN_POL");
+        return v ? (uint32_t)strtoul(v, nullptr, 0) : kPolDefault;
+    }();
     static bool attr = false;   // source blocks above 8192 senders / phase-M images need > 64 KiB of LDS
     if (!attr) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_scatter<double>),
@@ -684,18 +910,24 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
         float* st1 = reinterpret_cast<float*>(p.stage1);
         hipLaunchKernelGGL(k_bin_scatter<float>, dim3((p.P + 7) / 8 * 8 * p.segs), dim3(kBinA), p.SA * sizeof(float), s,
                            reinterpret_cast<const float*>(a.xin), p.idxA, p.aoff, st1, a.st, a.N, p.SA, p.segs,
-                           p.chunk);
+                           p.chunk, pol);
         const uint32_t nslot = a.nblk > p.Q ? a.nblk : p.Q;
         const uint32_t Qc = (nslot + 7) / 8;
         const dim3 grid(8 * Qc);
 #define X(DD, TT)                                                                                        \
     if (p.D == DD && a.trim == TT) {                                                                     \
-        if (a.rule == 4)                                                                                 \
+        if (p.ofree && a.rule == 4)                                                                      \
+            hipLaunchKernelGGL((k_bin_gather_of<DD, TT, true, float>), grid, dim3(kBinSB), 0, s, a, st1,    \
+                               p.rid, p.rstride, p.tiles, p.nrun, p.Q, Qc);                              \
+        else if (p.ofree)                                                                                \
+            hipLaunchKernelGGL((k_bin_gather_of<DD, TT, false, float>), grid, dim3(kBinSB), 0, s, a, st1,   \
+                               p.rid, p.rstride, p.tiles, p.nrun, p.Q, Qc);                              \
+        else if (a.rule == 4)                                                                            \
             hipLaunchKernelGGL((k_bin_gather<DD, TT, true, false, float>), grid, dim3(kBinSB), 0, s, a, st1, \
-                               p.invpos, p.tiles, p.nrun, p.Q, Qc);                                      \
+                               p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                      \
         else                                                                                             \
             hipLaunchKernelGGL((k_bin_gather<DD, TT, false, false, float>), grid, dim3(kBinSB), 0, s, a, st1, \
-                               p.invpos, p.tiles, p.nrun, p.Q, Qc);                                      \
+                               p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                      \
         return hipGetLastError();                                                                        \
     }
         ACS_BINNED_VARIANTS(X)
@@ -710,7 +942,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
         src = p.xtag;
     }
     hipLaunchKernelGGL(k_bin_scatter<double>, dim3((p.P + 7) / 8 * 8 * p.segs), dim3(kBinA), p.SA * sizeof(double), s, src, p.idxA, p.aoff,
-                       p.stage1, a.st, a.N, p.SA, p.segs, p.chunk);
+                       p.stage1, a.st, a.N, p.SA, p.segs, p.chunk, pol);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const double* last = p.stage1;
@@ -726,18 +958,24 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
 #define X(DD, TT)                                                                                        \
     if (p.D == DD && a.trim == TT) {                                                                     \
         const bool w_ = a.rule == 4;                                                                     \
-        if (clean && w_)                                                                                 \
+        if (clean && p.ofree && w_)                                                                      \
+            hipLaunchKernelGGL((k_bin_gather_of<DD, TT, true>), grid, dim3(kBinSB), 0, s, a, last, p.rid,   \
+                               p.rstride, p.tiles, p.nrun, p.Q, Qc);                                     \
+        else if (clean && p.ofree)                                                                       \
+            hipLaunchKernelGGL((k_bin_gather_of<DD, TT>), grid, dim3(kBinSB), 0, s, a, last, p.rid,         \
+                               p.rstride, p.tiles, p.nrun, p.Q, Qc);                                     \
+        else if (clean && w_)                                                                            \
             hipLaunchKernelGGL((k_bin_gather<DD, TT, true>), grid, dim3(kBinSB), 0, s, a, last, p.invpos,   \
-                               p.tiles, p.nrun, p.Q, Qc);                                                \
+                               p.tiles, p.nrun, p.Q, Qc, pol);                                                \
         else if (clean)                                                                                  \
             hipLaunchKernelGGL((k_bin_gather<DD, TT>), grid, dim3(kBinSB), 0, s, a, last, p.invpos, p.tiles, \
-                               p.nrun, p.Q, Qc);                                                         \
+                               p.nrun, p.Q, Qc, pol);                                                         \
         else if (w_)                                                                                     \
             hipLaunchKernelGGL((k_bin_gather<DD, TT, true, true>), grid, dim3(kBinSB), 0, s, a, last,       \
-                               p.invpos, p.tiles, p.nrun, p.Q, Qc);                                      \
+                               p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                      \
         else                                                                                             \
             hipLaunchKernelGGL((k_bin_gather<DD, TT, false, true>), grid, dim3(kBinSB), 0, s, a, last,      \
-                               p.invpos, p.tiles, p.nrun, p.Q, Qc);                                      \
+                               p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                      \
         return hipGetLastError();                                                                        \
     }
     ACS_BINNED_VARIANTS(X)
