@@ -125,6 +125,7 @@ struct BinnedPlan {
     uint16_t* invpos = nullptr;         // [Q][D/8][kBinSB][8]: position of (receiver, slot) in block b's runs
     uint2* tiles = nullptr;             // [Q][nrun+1] (stage start | pad count, element offset in block b's runs)
     bool ofree = false;                 // order-free phase B (rid, no invpos)
+    uint32_t pol = 0;                   // cache-policy switches (round_binned.hip kPol*)
     uint32_t rstride = 0;               // bytes per receiver block in rid
     uint8_t* rid = nullptr;             // [Q][rstride] receiver inside block b of each image position (ofree)
     uint2* mt = nullptr;                // [ngroups][PK+1] phase-M run tables (two levels)

@@ -848,6 +848,10 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
         e = hipGetLastError();
     }
     p.ofree = ofree;
+    {
+        const char* v = getenv("ACSIM_BIN_POL");
+        p.pol = v ? (uint32_t)strtoul(v, nullptr, 0) & 7u : kPolDefault;
+    }
     if (ofree) {   // order-free phase B: receiver ids in image order
         p.rstride = ((uint32_t)d * kBinSB + p.nrun * (G.pad - 1) + 15u) & ~15u;
         if (e == hipSuccess) e = hipMalloc(&p.rid, (uint64_t)G.Q * p.rstride);
@@ -888,10 +892,7 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
 }
 
 hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool clean, hipStream_t s) {
-    static const uint32_t pol = [] {
-        const char* v = getenv("ACSIM_BIN_POL");
-        return v ? (uint32_t)strtoul(v, nullptr, 0) : kPolDefault;
-    }();
+    const uint32_t pol = p.pol;
     static bool attr = false;   // source blocks above 8192 senders / phase-M images need > 64 KiB of LDS
     if (!attr) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_scatter<double>),

@@ -209,3 +209,48 @@ def test_faulty_chunks_resume_and_partitions(oracle_mod):
     with oracle_mod.OracleSimulator(cfg, threads=8) as o:
         o.run()
         assert int(o.rounds()[0]) == rounds and np.array_equal(bits(o.values(0)), ref)
+
+
+OF_CASES = ["d32_t5_eps_n50000_sa1024", "two_level_d16_t5_n100000_sa256", "d8_t2_midpoint_sa256",
+            "d32_t5_dlpsw_sa2048", "cfg4_shape_2e17"]
+
+
+@pytest.mark.parametrize("name", OF_CASES)
+def test_order_free_phase_b_matches_oracle(oracle_mod, name):
+    """ACSIM_BIN_OF=1: phase B places each receiver's values through LDS slot counters (order
+    varies, multiset does not); the sort-based rules must still agree bit for bit."""
+    cfg, sa = CASES[name]
+    with env(ACSIM_BIN_SA=sa, ACSIM_BIN_OF=1):
+        kb, rb, xb, tb = run_gpu(cfg)
+    assert kb.startswith("k_bin_scatter"), kb
+    with oracle_mod.OracleSimulator(cfg, threads=8) as o:
+        o.run()
+        assert np.array_equal(rb, o.rounds())
+        assert np.array_equal(xb, bits(o.values(0)))
+        assert np.array_equal(tb, bits(o.spread_trace(0)))
+
+
+def test_order_free_f32_and_wmsr(oracle_mod):
+    for cfg in (preset("cfg4_eps", n_nodes=1 << 16, dtype="f32", trace_spread=True),
+                Config(n_nodes=40000, topology="regular", degree=16, rule="wmsr", trim=5, eps=1e-9,
+                       max_rounds=200, seed=8, trace_spread=True)):
+        with env(ACSIM_BIN_OF=1, ACSIM_BIN_SA=2048):
+            with acsim.Simulator(cfg, device=0) as g:
+                assert g.kernel_name().startswith("k_bin_scatter")
+                g.run()
+                gr, gx = g.rounds(), g.values(0)
+        with oracle_mod.OracleSimulator(cfg, threads=8) as o:
+            o.run()
+            assert np.array_equal(gr, o.rounds())
+            assert np.array_equal(gx.view(np.uint8), o.values(0).view(np.uint8))
+
+
+@pytest.mark.parametrize("pol", [0, 1, 2, 7])
+def test_cache_policy_switches_bit_exact(oracle_mod, pol):
+    """ACSIM_BIN_POL only changes cache policies (nontemporal runs / stores / invpos loads)."""
+    cfg, sa = CASES["d32_t5_eps_n50000_sa1024"]
+    with env(ACSIM_BIN_SA=sa, ACSIM_BIN_POL=pol):
+        kb, rb, xb, tb = run_gpu(cfg)
+    with oracle_mod.OracleSimulator(cfg, threads=8) as o:
+        o.run()
+        assert np.array_equal(rb, o.rounds()) and np.array_equal(xb, bits(o.values(0)))
