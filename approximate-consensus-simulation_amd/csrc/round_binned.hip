@@ -166,7 +166,7 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
 __global__ __launch_bounds__(kBinA) void k_bin_regroup(const double* __restrict__ stage1, const uint2* __restrict__ mt,
                                                      const uint64_t* __restrict__ moff, const uint16_t* __restrict__ idxM,
                                                      double* __restrict__ stage2, const InstState* __restrict__ st,
-                                                     uint32_t PK) {
+                                                     uint32_t PK, uint32_t pol) {
     extern __shared__ double lm[];
     if (st->done) return;
     const uint32_t g = blockIdx.x;
@@ -174,7 +174,7 @@ __global__ __launch_bounds__(kBinA) void k_bin_regroup(const double* __restrict_
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     bin_dma_runs(mt + (uint64_t)g * (PK + 1), w * PK / NW, (w + 1) * PK / NW, stage1, lm);
     __syncthreads();
-    bin_stream(lm, idxM, stage2, moff[g], moff[g + 1]);
+    bin_stream(lm, idxM, stage2, moff[g], moff[g + 1], (pol & kPolNtStore) != 0);
 }
 
 // ------------------------------------------------------------------------------ phase B
@@ -949,7 +949,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
     const double* last = p.stage1;
     if (p.levels == 2) {
         hipLaunchKernelGGL(k_bin_regroup, dim3(p.ngroups), dim3(kBinA), (p.mcap + 2) * sizeof(double), s, p.stage1,
-                           p.mt, p.moff, p.idxM, p.stage2, a.st, p.PK);
+                           p.mt, p.moff, p.idxM, p.stage2, a.st, p.PK, pol);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         last = p.stage2;
     }
