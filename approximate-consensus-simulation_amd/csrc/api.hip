@@ -64,6 +64,10 @@ struct acs_sim {
     bool clean = true;
     bool ell_sorted = false;       // rows stored ascending (clean + order-independent rule)
     bool binned = false;           // PATH_REGULAR served by the binned exchange (round_binned.hip)
+    bool defer_fin = false;        // binned, one instance, unpartitioned: a round's finalize runs inside
+                                   // the next round's phase A (the last round of a chunk launches it)
+    bool fin_pending = false;
+    FinalizeArgs fin_args{};
     bool mfma = false;             // PATH_BATCHED served by the MFMA group kernel (batched_mfma.hip)
     bool dense_persist = false;    // PATH_DENSE served by the persistent LDS-resident kernel
     BinnedPlan bin{};
@@ -350,7 +354,8 @@ static int enqueue_round(acs_sim* s, uint32_t r) {
     if (rc) return rc;
     if (!s->partitioned) {
         if (s->binned) {
-            HIP_TRY(launch_round_binned(s->bin, a, s->clean, s->stream));
+            HIP_TRY(launch_round_binned(s->bin, a, s->clean, s->stream, s->fin_pending ? &s->fin_args : nullptr));
+            s->fin_pending = false;
         } else if (s->path == PATH_REGULAR) {
             HIP_TRY(launch_round_regular(a, s->B, s->clean, s->stream));
         } else if (s->path == PATH_DENSE) {
@@ -377,7 +382,13 @@ static int enqueue_round(acs_sim* s, uint32_t r) {
             HIP_TRY(launch_round_generic(a, s->B, s->stream));
         }
         if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
-        HIP_TRY(launch_finalize(make_finalize(s, r + 1, s->partial, s->nblk, false), s->B, s->stream));
+        const FinalizeArgs fin = make_finalize(s, r + 1, s->partial, s->nblk, false);
+        if (s->defer_fin) {   // folded by the next round's phase A, or by flush_finalize
+            s->fin_args = fin;
+            s->fin_pending = true;
+            return ACS_OK;
+        }
+        HIP_TRY(launch_finalize(fin, s->B, s->stream));
         return ACS_OK;
     }
     if (s->virt) {
@@ -451,6 +462,14 @@ static int read_states(acs_sim* s, std::vector<InstState>& out) {
 
 static constexpr uint32_t kChunk = 16;
 
+// Launch a finalize still deferred (the last round enqueued has no next phase A to fold it).
+static int flush_finalize(acs_sim* s) {
+    if (!s->fin_pending) return ACS_OK;
+    s->fin_pending = false;
+    HIP_TRY(launch_finalize(s->fin_args, s->B, s->stream));
+    return ACS_OK;
+}
+
 // Advance every unfinished instance by at most k rounds.
 static int advance(acs_sim* s, uint32_t k) {
     if (s->all_done || k == 0) return ACS_OK;
@@ -498,6 +517,7 @@ static int advance(acs_sim* s, uint32_t k) {
             int rc = enqueue_round(s, s->round + q);
             if (rc) return rc;
         }
+        if (int rc = flush_finalize(s)) return rc;
         s->round += chunk;
         k -= chunk;
         if (s->round >= s->c.max_rounds) break;
@@ -665,6 +685,8 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         s->binned = allow && (!s->f32 || (s->clean && lv == 1)) && s->path == PATH_REGULAR && cfg->delay_max == 0 &&
                     s->B == 1 && lv != 0 &&
                     binned_supported(s->d, cfg->trim, cfg->rule) && rows_local * s->d < (1ull << 32);
+        const char* df = getenv("ACSIM_DEFER_FIN");
+        s->defer_fin = s->binned && !partitioned && s->B == 1 && !(df && df[0] == '0');
         if (s->binned) {
             char nm[96];
             snprintf(nm, sizeof nm, "k_bin_scatter+%sk_bin_gather<%u,%u%s>%s", lv == 2 ? "k_bin_regroup+" : "", s->d,

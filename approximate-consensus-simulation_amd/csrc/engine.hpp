@@ -145,7 +145,9 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
                         uint32_t sa, bool tagged, bool f32, bool ofree, hipStream_t s);
 void binned_free(BinnedPlan& p);
 // clean: no slot-dependent decision (selects the plain phase-B instantiation)
-hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool clean, hipStream_t s);
+// fin: the previous round's finalize, deferred into this round's phase A (nullptr: none pending)
+hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool clean, hipStream_t s,
+                               const FinalizeArgs* fin = nullptr);
 
 // Generic kernel: one workgroup per receiver, LDS bitonic sort (any topology, m <= 8192).
 constexpr uint32_t kGenericMaxM = 8192;

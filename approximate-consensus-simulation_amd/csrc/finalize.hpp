@@ -29,9 +29,12 @@ __device__ __forceinline__ void store_partial_sc1(double2* p, double2 v) {
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <bool SC1>
-__device__ __forceinline__ void finalize_instance(const FinalizeArgs& a, uint32_t lb) {
-    constexpr uint32_t NT = 256;
+// Fold the block partials of instance lb and evaluate §A.8.  Called by all NT threads of a
+// workgroup; every thread returns the same verdict (done).  With `record`, thread 0 stores lo / hi /
+// spread / rounds / converged / done, the trace entry and the done counter (a partition fold
+// instead hands (-min, max) to fold_out and returns false).
+template <bool SC1, uint32_t NT = 256>
+__device__ __forceinline__ bool fold_partials(const FinalizeArgs& a, uint32_t lb, bool record) {
     InstState* S = a.st + lb;
     const double2* p = a.partial + (uint64_t)lb * a.nblk;
     double mn = kInf, mx = -kInf;
@@ -59,28 +62,34 @@ __device__ __forceinline__ void finalize_instance(const FinalizeArgs& a, uint32_
     mx = wave_max(mx);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = make_double2(mn, mx);
     __syncthreads();
-    if (threadIdx.x == 0) {
 #pragma unroll
-        for (uint32_t q = 0; q < NT / 64; ++q) {
-            mn = __builtin_fmin(mn, red[q].x);
-            mx = __builtin_fmax(mx, red[q].y);
-        }
-        if (a.fold_out) {   // node partition: hand (-min, max) to the all-reduce
-            *a.fold_out = make_double2(-mn, mx);
-            return;
-        }
-        const double spread = a.f32 ? (double)(float)(mx - mn) : mx - mn;   // binary32 subtraction
+    for (uint32_t q = 0; q < NT / 64; ++q) {
+        mn = __builtin_fmin(mn, red[q].x);
+        mx = __builtin_fmax(mx, red[q].y);
+    }
+    if (a.fold_out) {   // node partition: hand (-min, max) to the all-reduce
+        if (record && threadIdx.x == 0) *a.fold_out = make_double2(-mn, mx);
+        return false;
+    }
+    const double spread = a.f32 ? (double)(float)(mx - mn) : mx - mn;   // binary32 subtraction
+    const bool conv = spread <= a.eps;
+    const bool done = (a.term_eps && conv) || a.r_next >= a.max_rounds;
+    if (record && threadIdx.x == 0) {
         S->lo = mn;
         S->hi = mx;
         S->spread = spread;
         S->rounds = a.r_next;
-        const bool conv = spread <= a.eps;
-        const bool done = (a.term_eps && conv) || a.r_next >= a.max_rounds;
         S->converged = conv ? 1u : 0u;
         S->done = done ? 1u : 0u;
         if (a.trace) a.trace[(uint64_t)lb * a.trace_stride + a.r_next] = spread;
         if (done) atomicAdd(a.n_done, 1u);
     }
+    return done;
+}
+
+template <bool SC1>
+__device__ __forceinline__ void finalize_instance(const FinalizeArgs& a, uint32_t lb) {
+    (void)fold_partials<SC1>(a, lb, true);
 }
 
 }  // namespace acs

@@ -35,6 +35,7 @@
 
 #include <vector>
 
+#include "finalize.hpp"
 #include "resolve.hpp"
 #include "rules.hpp"
 
@@ -131,7 +132,8 @@ template <typename VT = double>
 __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x, const uint16_t* __restrict__ idxA,
                                                      const uint64_t* __restrict__ aoff, VT* __restrict__ stage,
                                                      const InstState* __restrict__ st, uint64_t N, uint32_t SA,
-                                                     uint32_t segs, uint32_t chunk, uint32_t pol) {
+                                                     uint32_t segs, uint32_t chunk, uint32_t pol,
+                                                     const FinalizeArgs fin, uint32_t fin_on) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lx_raw[];
     VT* lx = reinterpret_cast<VT*>(lx_raw);
     if (st->done) return;
@@ -140,13 +142,15 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
     // instead of once per XCD.  The grid is 8 * ceil(P / 8) * segs.
     const uint32_t slot = blockIdx.x >> 3;
     const uint32_t a = (slot / segs) * 8 + (blockIdx.x & 7u), sg = slot % segs;
-    if ((uint64_t)a * SA >= N) return;   // padding past the last source block
-    const uint64_t pa1 = aoff[a + 1];
-    const uint64_t p0 = aoff[a] + (uint64_t)sg * chunk;
-    if (p0 >= pa1) return;
+    // padding past the last source block, or a segment past its block's deliveries: idle (but
+    // workgroup 0 still records a deferred finalize)
+    const bool idle = (uint64_t)a * SA >= N || aoff[a] + (uint64_t)sg * chunk >= aoff[a + 1];
+    if (idle && !(fin_on && blockIdx.x == 0)) return;
+    const uint64_t pa1 = idle ? 0 : aoff[a + 1];
+    const uint64_t p0 = idle ? 0 : aoff[a] + (uint64_t)sg * chunk;
     const uint64_t p1 = p0 + chunk < pa1 ? p0 + chunk : pa1;
     const uint64_t base = (uint64_t)a * SA;
-    const uint32_t n = (uint32_t)(N - base < SA ? N - base : SA);
+    const uint32_t n = idle ? 0u : (uint32_t)(N - base < SA ? N - base : SA);
     {   // x block -> LDS by LDS-DMA, 16 B per lane (x is allocated with spare elements, so the
         // last odd element's pair never reads past the buffer)
         constexpr uint32_t EPU = 16 / sizeof(VT);
@@ -156,7 +160,23 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
         for (uint32_t o = 0; o < n16; o += kBinA)
             if (o + threadIdx.x < n16) __builtin_amdgcn_global_load_lds(xs + o, ld + o, 16, 0, 0);
     }
-    __syncthreads();
+    if (fin_on) {
+        // deferred finalize of the previous round.  Workgroup 0 folds the
+        // partials and records the verdict (the loads overlap the x staging above; the fold's
+        // barrier drains both).  Under EPS termination every workgroup folds them too and reaches
+        // the same verdict; under FIXED termination the verdict is the round count alone.  A
+        // finished instance stops here.
+        bool done;
+        if (fin.term_eps || blockIdx.x == 0) {
+            done = fold_partials<false, kBinA>(fin, 0, blockIdx.x == 0);
+        } else {
+            __syncthreads();
+            done = fin.r_next >= fin.max_rounds;
+        }
+        if (done || idle) return;
+    } else {
+        __syncthreads();
+    }
     bin_stream(lx, idxA, stage, p0, p1, (pol & kPolNtStore) != 0);
 }
 
@@ -891,7 +911,10 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     return e;
 }
 
-hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool clean, hipStream_t s) {
+hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool clean, hipStream_t s,
+                               const FinalizeArgs* fin) {
+    const FinalizeArgs fa = fin ? *fin : FinalizeArgs{};
+    const uint32_t fin_on = fin ? 1u : 0u;
     const uint32_t pol = p.pol;
     static bool attr = false;   // source blocks above 8192 senders / phase-M images need > 64 KiB of LDS
     if (!attr) {
@@ -911,7 +934,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
         float* st1 = reinterpret_cast<float*>(p.stage1);
         hipLaunchKernelGGL(k_bin_scatter<float>, dim3((p.P + 7) / 8 * 8 * p.segs), dim3(kBinA), p.SA * sizeof(float), s,
                            reinterpret_cast<const float*>(a.xin), p.idxA, p.aoff, st1, a.st, a.N, p.SA, p.segs,
-                           p.chunk, pol);
+                           p.chunk, pol, fa, fin_on);
         const uint32_t nslot = a.nblk > p.Q ? a.nblk : p.Q;
         const uint32_t Qc = (nslot + 7) / 8;
         const dim3 grid(8 * Qc);
@@ -943,7 +966,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
         src = p.xtag;
     }
     hipLaunchKernelGGL(k_bin_scatter<double>, dim3((p.P + 7) / 8 * 8 * p.segs), dim3(kBinA), p.SA * sizeof(double), s, src, p.idxA, p.aoff,
-                       p.stage1, a.st, a.N, p.SA, p.segs, p.chunk, pol);
+                       p.stage1, a.st, a.N, p.SA, p.segs, p.chunk, pol, fa, fin_on);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const double* last = p.stage1;
