@@ -12,7 +12,9 @@ The roofline object prices the dominant kernel at SURVEY §8(d)'s algorithmic 40
 launch processes, divided by its average device duration measured with HIP events on the
 handle's stream over the timed region.  On cfg4 the round is the binned exchange
 (csrc/round_binned.hip): two launches, k_bin_scatter then k_bin_gather, bracketed together by
-one event pair, so "one launch" here means that pair (the ε finalize is excluded).  Every
+one event pair, so "one launch" here means that pair.  The ε-spread fold of the previous round runs
+inside k_bin_scatter (deferred finalize) and is therefore included; the one
+standalone k_finalize per 16-round chunk is not.  Every
 --event-every-th timed round (default 10) is bracketed: an event pair idles the stream for
 ~5 µs, which would otherwise inflate ms_per_step by ~7 %.
 `traffic` is the pair's measured HBM bytes per round (profiles/pmc_cfg4.json, FETCH_SIZE x 2 +
