@@ -492,6 +492,7 @@ static int advance(acs_sim* s, uint32_t k) {
         a.term_eps = s->c.termination == ACS_TERM_EPS;
         a.eps = s->c.eps;
         a.mp = s->mp;
+        a.f32 = s->f32 ? 1u : 0u;
         hipEvent_t e1;
         int rc = timing_begin(s, &e1);
         if (rc) return rc;
@@ -630,13 +631,13 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
 
     s->f32 = cfg->dtype == ACS_F32;
     s->es = s->f32 ? 4u : 8u;
-    // fp32 runs on the register and generic kernels; the batched, MFMA, dense and
-    // binned fast paths are fp64-only
-    if (cfg->topology == ACS_TOPO_COMPLETE && s->N <= kBatchedMaxN && cfg->delay_max == 0 && !s->f32) {
+    // fp32 runs on the register, generic, batched (N <= 64) and one-level binned
+    // kernels; the MFMA and dense fast paths are fp64-only
+    if (cfg->topology == ACS_TOPO_COMPLETE && s->N <= kBatchedMaxN && cfg->delay_max == 0) {
         s->path = PATH_BATCHED;
         s->kname = batched_small_name((uint32_t)s->N, cfg->rule, cfg->fault_model != ACS_FAULT_NONE);
         const char* env = getenv("ACSIM_MFMA");
-        s->mfma = !(env && env[0] == '0') &&
+        s->mfma = !(env && env[0] == '0') && !s->f32 &&
                   batched_mfma_supported((uint32_t)s->N, cfg->rule, cfg->fault_model != ACS_FAULT_NONE, cfg->mask_group,
                                          cfg->instance_offset);
         if (s->mfma) s->kname = "k_batched_mfma<v_mfma_f64_16x16x4>";

@@ -33,8 +33,8 @@ constexpr int ilog2(int p) {
     return l;
 }
 
-template <int P, int Q, int LOG2P>
-__device__ __forceinline__ void push_leaf(double (&acc)[LOG2P + 1], double v) {
+template <int P, int Q, int LOG2P, typename VT>
+__device__ __forceinline__ void push_leaf(VT (&acc)[LOG2P + 1], VT v) {
     // combine while bit l of Q is set (compile-time), then park at level l
     if constexpr ((Q & 1) && LOG2P > 0) {
         v = acc[0] + v;
@@ -59,26 +59,33 @@ __device__ __forceinline__ void push_leaf(double (&acc)[LOG2P + 1], double v) {
     }
 }
 
+template <typename VT>
 struct LaneCtx {
     const MsgParams* mp;
     uint32_t N, lane, b, r;
-    double xi, lo, hi;
+    VT xi, lo, hi;
     uint32_t sti;
     uint64_t miss;   // bit j: message from j missing (crash or drop)
 };
 
 // Byzantine value kept out of line: inlined into each of the P unrolled leaves it multiplied the
 // code (one Philox call per leaf) and spilled registers.
-__device__ __noinline__ double byz_value_ool(const MsgParams& mp, uint32_t b, uint32_t r, uint32_t i, uint64_t s,
-                                             double lo, double hi) {
-    return byz_value(mp, b, r, i, s, lo, hi);
+template <typename VT>
+__device__ __noinline__ VT byz_value_ool(const MsgParams& mp, uint32_t b, uint32_t r, uint32_t i, uint64_t s, VT lo,
+                                         VT hi) {
+    return byz_value_t(mp, b, r, i, s, lo, hi);   // binary32 arithmetic for float
+}
+
+__device__ __forceinline__ double readlane_v(double v, int lane) { return readlane_f64(v, lane); }
+__device__ __forceinline__ float readlane_v(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
 
 // §A.6 entry j of receiver `lane` (valid for j < N).  FAULTS = false: no fault schedule, so a
 // sender is never Byzantine and only the drop bits matter (cfg3).
-template <bool FAULTS>
-__device__ __forceinline__ double entry_value(const LaneCtx& c, int j) {
-    const double xj = readlane_f64(c.xi, j);
+template <bool FAULTS, typename VT>
+__device__ __forceinline__ VT entry_value(const LaneCtx<VT>& c, int j) {
+    const VT xj = readlane_v(c.xi, j);
     if ((uint32_t)j == c.lane) return c.xi;
     if ((c.miss >> j) & 1ull) return c.xi;
     if constexpr (FAULTS) {
@@ -88,15 +95,17 @@ __device__ __forceinline__ double entry_value(const LaneCtx& c, int j) {
     return xj;
 }
 
-template <int P, bool FAULTS, int... Q>
-__device__ __forceinline__ double average_tree(const LaneCtx& c, std::integer_sequence<int, Q...>) {
+template <int P, bool FAULTS, typename VT, int... Q>
+__device__ __forceinline__ VT average_tree(const LaneCtx<VT>& c, std::integer_sequence<int, Q...>) {
     constexpr int LOG2P = ilog2(P);
-    double acc[LOG2P + 1];
-    (push_leaf<P, Q, LOG2P>(acc, (bitrev<LOG2P>(Q) < (int)c.N) ? entry_value<FAULTS>(c, bitrev<LOG2P>(Q)) : 0.0), ...);
+    VT acc[LOG2P + 1];
+    (push_leaf<P, Q, LOG2P>(acc, (bitrev<LOG2P>(Q) < (int)c.N) ? entry_value<FAULTS>(c, bitrev<LOG2P>(Q)) : VT(0)), ...);
     return acc[LOG2P];
 }
 
-template <int P, bool SORT, bool FAULTS>
+// VT = double, or float in fp32 mode: every §A.7 step in binary32, spread =
+// binary32(hi - lo) compared as a double, lo / hi / spread kept as doubles in InstState.
+template <int P, bool SORT, bool FAULTS, typename VT = double>
 __global__ __launch_bounds__(64) void k_batched_small(const BatchArgs a, uint32_t kmax) {
     const uint32_t lb = blockIdx.x;
     const uint32_t lane = threadIdx.x;
@@ -109,16 +118,16 @@ __global__ __launch_bounds__(64) void k_batched_small(const BatchArgs a, uint32_
     const uint32_t b = (uint32_t)(mp.inst_offset + lb);
     const uint32_t bG = b - b % mp.mask_group;
     const bool valid = lane < N;
-    const double* xin = ((r & 1u) ? a.x1 : a.x0) + (uint64_t)lb * N;
-    double xi = valid ? xin[lane] : 0.0;
+    const VT* xin = reinterpret_cast<const VT*>((r & 1u) ? a.x1 : a.x0) + (uint64_t)lb * N;
+    VT xi = valid ? xin[lane] : VT(0);
     const uint32_t sti = valid ? (a.status ? a.status[(uint64_t)lb * N + lane] : kHonest) : kByz;
     const bool honest = sti == kHonest;
-    __shared__ double colbuf[SORT ? P * 64 : 1];
+    __shared__ VT colbuf[SORT ? P * 64 : 1];
     bool done = false, conv = spread <= a.eps;
     for (uint32_t q = 0; q < kmax; ++q) {
         const bool act = valid && is_active(sti, r);
-        LaneCtx c;
-        c.mp = &mp; c.N = N; c.lane = lane; c.b = b; c.r = r; c.xi = xi; c.lo = lo; c.hi = hi;
+        LaneCtx<VT> c;
+        c.mp = &mp; c.N = N; c.lane = lane; c.b = b; c.r = r; c.xi = xi; c.lo = (VT)lo; c.hi = (VT)hi;
         c.sti = sti;
         c.miss = 0;
         // drop mask (§A.5): slot s = lane*N + j
@@ -144,26 +153,26 @@ __global__ __launch_bounds__(64) void k_batched_small(const BatchArgs a, uint32_
                     c.miss |= 1ull << j;
             }
         }
-        double res;
+        VT res;
         if constexpr (!SORT) {
-            res = average_tree<P, FAULTS>(c, std::make_integer_sequence<int, P>{}) / (double)N;
+            res = average_tree<P, FAULTS>(c, std::make_integer_sequence<int, P>{}) / (VT)N;
         } else {
-            double v[P];
+            VT v[P];
 #pragma unroll
-            for (int j = 0; j < P; ++j) v[j] = j < (int)N ? entry_value<FAULTS>(c, j) : kInf;
+            for (int j = 0; j < P; ++j) v[j] = j < (int)N ? entry_value<FAULTS>(c, j) : (VT)kInf;
             select_sort<P>(v);
 #pragma unroll
             for (int k = 0; k < P; ++k) colbuf[k * 64 + lane] = v[k];
             const uint32_t t = a.trim, nr = N - 2 * t;
             if (a.rule == 2) {
-                res = (colbuf[t * 64 + lane] + colbuf[(N - t - 1) * 64 + lane]) * 0.5;
+                res = (colbuf[t * 64 + lane] + colbuf[(N - t - 1) * 64 + lane]) * VT(0.5);
             } else {
                 uint32_t start = t, step = a.rule == 3 ? t : 1;
                 uint32_t cnt = a.rule == 3 ? (nr + t - 1) / t : nr;
                 if (a.rule == 4) {   // W-MSR: window [min(t, #below), N - min(t, #above))
                     uint32_t nl = 0, ng = 0;
                     for (uint32_t k = 0; k < N; ++k) {
-                        const double u = colbuf[k * 64 + lane];
+                        const VT u = colbuf[k * 64 + lane];
                         nl += u < xi;
                         ng += u > xi;
                     }
@@ -175,24 +184,24 @@ __global__ __launch_bounds__(64) void k_batched_small(const BatchArgs a, uint32_
                 uint32_t P2 = 1;
                 while (P2 < cnt) P2 <<= 1;
                 for (uint32_t k = 0; k < P2; ++k)   // in place: source index start + k*step >= k
-                    colbuf[k * 64 + lane] = k < cnt ? colbuf[(start + k * step) * 64 + lane] : 0.0;
+                    colbuf[k * 64 + lane] = k < cnt ? colbuf[(start + k * step) * 64 + lane] : VT(0);
                 for (uint32_t s2 = P2 >> 1; s2 >= 1; s2 >>= 1)
                     for (uint32_t k = 0; k < s2; ++k)
                         colbuf[k * 64 + lane] = colbuf[k * 64 + lane] + colbuf[(k + s2) * 64 + lane];
-                res = colbuf[lane] / (double)cnt;
+                res = colbuf[lane] / (VT)cnt;
             }
         }
         xi = act ? res : xi;
         r += 1;
-        lo = wave_min(honest ? xi : kInf);
-        hi = wave_max(honest ? xi : -kInf);
-        spread = hi - lo;
+        lo = wave_min(honest ? (double)xi : kInf);
+        hi = wave_max(honest ? (double)xi : -kInf);
+        spread = (double)((VT)hi - (VT)lo);   // binary32 subtraction in fp32 mode
         if (a.trace && lane == 0) a.trace[(uint64_t)lb * a.trace_stride + r] = spread;
         conv = spread <= a.eps;
         done = (a.term_eps && conv) || r >= a.max_rounds;
         if (done) break;
     }
-    double* xout = ((r & 1u) ? a.x1 : a.x0) + (uint64_t)lb * N;
+    VT* xout = reinterpret_cast<VT*>((r & 1u) ? a.x1 : a.x0) + (uint64_t)lb * N;
     if (valid) xout[lane] = xi;
     if (lane == 0) {
         S->lo = lo;
@@ -219,17 +228,17 @@ const char* batched_small_name(uint32_t N, uint32_t rule, bool faults) {
     return nm;
 }
 
-hipError_t launch_batched_small(const BatchArgs& a, uint64_t B, uint32_t k, hipStream_t s) {
-    if (a.N < 1 || a.N > kBatchedMaxN) return hipErrorNotSupported;
+template <typename VT>
+static hipError_t launch_batched_small_t(const BatchArgs& a, uint64_t B, uint32_t k, hipStream_t s) {
     const int P = pick_p(a.N);
     const bool sort = a.rule != 0, faults = a.status != nullptr;
     const dim3 grid((unsigned)B), block(64);
-#define L(PP)                                                                                        \
-    case PP:                                                                                         \
-        if (sort && faults) hipLaunchKernelGGL((k_batched_small<PP, true, true>), grid, block, 0, s, a, k);   \
-        else if (sort) hipLaunchKernelGGL((k_batched_small<PP, true, false>), grid, block, 0, s, a, k);       \
-        else if (faults) hipLaunchKernelGGL((k_batched_small<PP, false, true>), grid, block, 0, s, a, k);     \
-        else hipLaunchKernelGGL((k_batched_small<PP, false, false>), grid, block, 0, s, a, k);                \
+#define L(PP)                                                                                                  \
+    case PP:                                                                                                   \
+        if (sort && faults) hipLaunchKernelGGL((k_batched_small<PP, true, true, VT>), grid, block, 0, s, a, k);   \
+        else if (sort) hipLaunchKernelGGL((k_batched_small<PP, true, false, VT>), grid, block, 0, s, a, k);       \
+        else if (faults) hipLaunchKernelGGL((k_batched_small<PP, false, true, VT>), grid, block, 0, s, a, k);     \
+        else hipLaunchKernelGGL((k_batched_small<PP, false, false, VT>), grid, block, 0, s, a, k);                \
         break;
     switch (P) {
         L(2) L(4) L(8) L(16) L(32) L(64)
@@ -237,6 +246,11 @@ hipError_t launch_batched_small(const BatchArgs& a, uint64_t B, uint32_t k, hipS
     }
 #undef L
     return hipGetLastError();
+}
+
+hipError_t launch_batched_small(const BatchArgs& a, uint64_t B, uint32_t k, hipStream_t s) {
+    if (a.N < 1 || a.N > kBatchedMaxN) return hipErrorNotSupported;
+    return a.f32 ? launch_batched_small_t<float>(a, B, k, s) : launch_batched_small_t<double>(a, B, k, s);
 }
 
 }  // namespace acs

@@ -80,6 +80,7 @@ struct BatchArgs {
     uint32_t N, rule, trim, max_rounds, term_eps;
     double eps;
     MsgParams mp;
+    uint32_t f32;             // values are binary32 (batched_small.hip only)
 };
 
 // ---- setup kernels (setup.hip)

@@ -28,14 +28,26 @@ CASES = {
                                   fault_model="byzantine", n_faulty=10, byz_strategy="constant",
                                   byz_const=0.7, loss_p=0.05, delay_max=3, eps=1e-6, max_rounds=300,
                                   seed=16, trace_spread=True, dtype="f32"),
-    # generic kernel: complete graph, midpoint, crash + loss (cfg1-like)
+    # batched wavefront kernel (N <= 64): complete graph, midpoint, crash + loss (cfg1-like)
     "complete_mid_crash_drop": Config(n_nodes=50, topology="complete", rule="midpoint", trim=4,
                                       fault_model="crash", n_faulty=6, crash_window=3, loss_p=0.15,
                                       eps=1e-6, max_rounds=200, seed=21, trace_spread=True, dtype="f32"),
-    # generic kernel: batched averaging instances with grouped drop masks (cfg3-like)
+    # batched wavefront kernel: averaging instances with grouped drop masks (cfg3-like)
     "complete_avg_batched": Config(n_nodes=64, n_instances=40, topology="complete", rule="average",
                                    loss_p=0.2, mask_group=4, eps=1e-6, max_rounds=100, seed=2,
                                    dtype="f32"),
+    # batched wavefront kernel: the cfg1 presets and a cfg3 slice in binary32
+    "cfg1_f32": preset("cfg1", dtype="f32", trace_spread=True),
+    "cfg1_avg_f32": preset("cfg1_avg", dtype="f32", trace_spread=True),
+    "cfg3_slice_f32": preset("cfg3", n_instances=3000, dtype="f32", trace_spread=True),
+    # batched wavefront kernel: Byzantine RANDOM, DLPSW and W-MSR on small complete graphs
+    "complete_byzrandom_dlpsw": Config(n_nodes=40, n_instances=16, topology="complete", rule="dlpsw", trim=6,
+                                       fault_model="byzantine", n_faulty=6, byz_strategy="random",
+                                       byz_delta=0.1, loss_p=0.1, eps=1e-6, max_rounds=300, seed=31,
+                                       trace_spread=True, dtype="f32"),
+    "complete_wmsr_split": Config(n_nodes=33, n_instances=8, topology="complete", rule="wmsr", trim=5,
+                                  fault_model="byzantine", n_faulty=5, byz_strategy="split", byz_delta=0.2,
+                                  eps=1e-6, max_rounds=300, seed=32, trace_spread=True, dtype="f32"),
     # generic kernel: Byzantine SPLIT trimmed mean on a complete graph (cfg2-like, smaller)
     "complete_trimmed_split": Config(n_nodes=256, topology="complete", rule="trimmed", trim=85,
                                      fault_model="byzantine", n_faulty=85, byz_strategy="split",
@@ -52,7 +64,14 @@ def test_f32_matches_oracle(oracle_mod, name):
     g, o = run_both(oracle_mod, cfg)
     assert g["x"].dtype == np.float32 and o["x"].dtype == np.float32
     assert_same(g, o)
-    assert int(g["rounds"].max()) > 2
+    assert int(g["rounds"].max()) > (0 if name.startswith("cfg1") else 2)   # cfg1 MIDPOINT converges in 1
+
+
+def test_f32_small_complete_graphs_take_the_batched_kernel():
+    for name in ("cfg1_f32", "cfg1_avg_f32", "cfg3_slice_f32", "complete_avg_batched"):
+        with acsim.Simulator(CASES[name], device=0) as g:
+            assert g.kernel_name().startswith("k_batched_small<"), (name, g.kernel_name())
+            assert g.kernel_name().endswith("[f32]")
 
 
 def test_f32_resume_and_chunks(oracle_mod):

@@ -24,6 +24,7 @@ CASES = {
     "cfg4_byz": dict(),
     "cfg5": dict(max_rounds=20),
     "cfg4_f32": dict(max_rounds=100),   # fp32 mode
+    "cfg3_f32": dict(),
 }
 
 
