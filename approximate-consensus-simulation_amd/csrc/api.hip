@@ -631,8 +631,8 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
 
     s->f32 = cfg->dtype == ACS_F32;
     s->es = s->f32 ? 4u : 8u;
-    // fp32 runs on the register, generic, batched (N <= 64) and one-level binned
-    // kernels; the MFMA and dense fast paths are fp64-only
+    // fp32 runs on the register, generic, batched (N <= 64), persistent dense
+    // (N <= 4096) and one-level binned kernels; the MFMA and two-kernel dense paths are fp64-only
     if (cfg->topology == ACS_TOPO_COMPLETE && s->N <= kBatchedMaxN && cfg->delay_max == 0) {
         s->path = PATH_BATCHED;
         s->kname = batched_small_name((uint32_t)s->N, cfg->rule, cfg->fault_model != ACS_FAULT_NONE);
@@ -641,8 +641,9 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
                   batched_mfma_supported((uint32_t)s->N, cfg->rule, cfg->fault_model != ACS_FAULT_NONE, cfg->mask_group,
                                          cfg->instance_offset);
         if (s->mfma) s->kname = "k_batched_mfma<v_mfma_f64_16x16x4>";
-    } else if (cfg->topology == ACS_TOPO_COMPLETE && !partitioned && cfg->delay_max == 0 && !s->f32 &&
-               (s->B == 1 || (s->N <= kDensePersistMaxN && !env_off("ACSIM_DENSE_PERSIST"))) &&
+    } else if (cfg->topology == ACS_TOPO_COMPLETE && !partitioned && cfg->delay_max == 0 &&
+               (s->f32 ? s->N <= kDensePersistMaxN && !env_off("ACSIM_DENSE_PERSIST")   // fp32: persistent only
+                       : (s->B == 1 || (s->N <= kDensePersistMaxN && !env_off("ACSIM_DENSE_PERSIST")))) &&
                dense_supported(cfg->fault_model, cfg->byz_strategy, cfg->rule, s->mp.thr, s->N)) {
         s->path = PATH_DENSE;
         s->dense_persist = s->N <= kDensePersistMaxN && !env_off("ACSIM_DENSE_PERSIST");

@@ -76,10 +76,6 @@ __device__ __noinline__ VT byz_value_ool(const MsgParams& mp, uint32_t b, uint32
     return byz_value_t(mp, b, r, i, s, lo, hi);   // binary32 arithmetic for float
 }
 
-__device__ __forceinline__ double readlane_v(double v, int lane) { return readlane_f64(v, lane); }
-__device__ __forceinline__ float readlane_v(float v, int lane) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
-}
 
 // §A.6 entry j of receiver `lane` (valid for j < N).  FAULTS = false: no fault schedule, so a
 // sender is never Byzantine and only the drop bits matter (cfg3).

@@ -72,5 +72,9 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
     const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
     return __hiloint2double(hi, lo);
 }
+__device__ __forceinline__ double readlane_v(double v, int lane) { return readlane_f64(v, lane); }
+__device__ __forceinline__ float readlane_v(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
 
 }  // namespace acs

@@ -27,14 +27,20 @@ constexpr int kDenseRecvBlock = 256;   // 4 receivers (wavefronts) per block
 // wavefront (shuffle, no barrier); 64 <= j < 1024: partner in another wavefront (LDS exchange,
 // one barrier pair); j >= 1024: partner in the same thread (register swap).  55 stages at
 // P = 1024, of which only 10 touch LDS.
-template <int EMAX>
-__device__ __forceinline__ void dense_bitonic(double* sh, uint32_t P, double (&v)[EMAX]) {
+__device__ __forceinline__ double vmin(double a, double b) { return __builtin_fmin(a, b); }
+__device__ __forceinline__ double vmax(double a, double b) { return __builtin_fmax(a, b); }
+__device__ __forceinline__ float vmin(float a, float b) { return __builtin_fminf(a, b); }
+__device__ __forceinline__ float vmax(float a, float b) { return __builtin_fmaxf(a, b); }
+
+// VT = double, or float for the fp32 persistent kernel
+template <int EMAX, typename VT>
+__device__ __forceinline__ void dense_bitonic(VT* sh, uint32_t P, VT (&v)[EMAX]) {
     const uint32_t E = (P + kDenseSortBlock - 1) / kDenseSortBlock;
     const uint32_t tid = threadIdx.x;
 #pragma unroll
     for (int e = 0; e < EMAX; ++e) {
         const uint32_t idx = tid + kDenseSortBlock * e;
-        v[e] = ((uint32_t)e < E && idx < P) ? sh[idx] : kInf;
+        v[e] = ((uint32_t)e < E && idx < P) ? sh[idx] : (VT)kInf;
     }
     __syncthreads();
     for (uint32_t k = 2; k <= P; k <<= 1) {
@@ -44,9 +50,9 @@ __device__ __forceinline__ void dense_bitonic(double* sh, uint32_t P, double (&v
                 for (int e = 0; e < EMAX; ++e) {
                     if ((uint32_t)e >= E) break;
                     const uint32_t idx = tid + kDenseSortBlock * e;
-                    const double p = __shfl_xor(v[e], (int)j, 64);
+                    const VT p = __shfl_xor(v[e], (int)j, 64);
                     const bool keep_min = ((idx & j) == 0) == ((idx & k) == 0);
-                    v[e] = keep_min ? __builtin_fmin(v[e], p) : __builtin_fmax(v[e], p);
+                    v[e] = keep_min ? vmin(v[e], p) : vmax(v[e], p);
                 }
             } else if (j < (uint32_t)kDenseSortBlock) {
 #pragma unroll
@@ -57,9 +63,9 @@ __device__ __forceinline__ void dense_bitonic(double* sh, uint32_t P, double (&v
                 for (int e = 0; e < EMAX; ++e) {
                     if ((uint32_t)e >= E) break;
                     const uint32_t idx = tid + kDenseSortBlock * e;
-                    const double p = sh[idx ^ j];
+                    const VT p = sh[idx ^ j];
                     const bool keep_min = ((idx & j) == 0) == ((idx & k) == 0);
-                    v[e] = keep_min ? __builtin_fmin(v[e], p) : __builtin_fmax(v[e], p);
+                    v[e] = keep_min ? vmin(v[e], p) : vmax(v[e], p);
                 }
                 __syncthreads();
             } else {
@@ -68,7 +74,7 @@ __device__ __forceinline__ void dense_bitonic(double* sh, uint32_t P, double (&v
     _Pragma("unroll") for (int e = 0; e < EMAX; ++e) {                                          \
         if ((e ^ EJ) > e && (uint32_t)(e ^ EJ) < E) {                                           \
             const uint32_t idx = tid + kDenseSortBlock * e;                                     \
-            const double lo_ = __builtin_fmin(v[e], v[e ^ EJ]), hi_ = __builtin_fmax(v[e], v[e ^ EJ]); \
+            const VT lo_ = vmin(v[e], v[e ^ EJ]), hi_ = vmax(v[e], v[e ^ EJ]);                 \
             const bool asc = (idx & k) == 0;                                                    \
             v[e] = asc ? lo_ : hi_;                                                             \
             v[e ^ EJ] = asc ? hi_ : lo_;                                                        \
@@ -138,7 +144,8 @@ __global__ __launch_bounds__(kDenseSortBlock) void k_dense_sort(const DenseArgs 
 }
 
 // number of elements of sorted b[0..n) strictly below v
-__device__ __forceinline__ uint32_t rank_below(const double* b, uint32_t n, double v) {
+template <typename VT>
+__device__ __forceinline__ uint32_t rank_below(const VT* b, uint32_t n, VT v) {
     uint32_t lo = 0, hi = n;
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -148,11 +155,13 @@ __device__ __forceinline__ uint32_t rank_below(const double* b, uint32_t n, doub
     return lo;
 }
 
+template <typename VT = double>
 struct Merged {   // M = B with two constant blocks (v1 <= v2) spliced in at their ranks
-    const double* b;
+    using value_type = VT;
+    const VT* b;
     uint32_t r1, n1, r2, n2;
-    double v1, v2;
-    __device__ __forceinline__ double at(uint32_t k) const {
+    VT v1, v2;
+    __device__ __forceinline__ VT at(uint32_t k) const {
         if (k < r1) return b[k];
         if (k < r1 + n1) return v1;
         if (k < r2 + n1) return b[k - n1];
@@ -164,20 +173,22 @@ struct Merged {   // M = B with two constant blocks (v1 <= v2) spliced in at the
 // A sorted sequence made of three constant runs: v[0] on [0, e[0]), v[1] on [e[0], e[1]), v[2] on
 // [e[1], m).  After one persistent round every active node holds its class value, so a
 // receiver's sequence is the class values of the base plus its Byzantine block: three runs.
+template <typename VT = double>
 struct Runs3 {
-    double v[3];
+    using value_type = VT;
+    VT v[3];
     uint32_t e[2];
-    __device__ __forceinline__ double at(uint32_t k) const { return k < e[0] ? v[0] : k < e[1] ? v[1] : v[2]; }
+    __device__ __forceinline__ VT at(uint32_t k) const { return k < e[0] ? v[0] : k < e[1] ? v[1] : v[2]; }
 };
 
 // The rule over the window R = M[t, m - t) of one receiver's merged sorted sequence, by one
 // wavefront (§A.7 stride-halving tree sum spread over the 64 lanes); every lane returns the result.
-template <typename Seq>
-__device__ __forceinline__ double dense_window(const Seq& M, uint32_t rule, uint32_t m, uint32_t t, uint32_t lane) {
+template <typename Seq, typename VT = typename Seq::value_type>
+__device__ __forceinline__ VT dense_window(const Seq& M, uint32_t rule, uint32_t m, uint32_t t, uint32_t lane) {
     const uint32_t nr = m - 2 * t;
-    double res;
+    VT res;
     if (rule == 2) {
-        res = (M.at(t) + M.at(m - t - 1)) * 0.5;
+        res = (M.at(t) + M.at(m - t - 1)) * VT(0.5);
     } else {
         const uint32_t step = rule == 3 ? t : 1;
         const uint32_t cnt = rule == 3 ? (nr + t - 1) / t : nr;
@@ -185,17 +196,15 @@ __device__ __forceinline__ double dense_window(const Seq& M, uint32_t rule, uint
         while (P2 < cnt) P2 <<= 1;
         // §A.7 stride halving over P2 slots: this lane owns w[lane + 64a]
         const uint32_t per = P2 / 64;   // <= 128 for m <= 8192
-        double w[8];
+        VT w[8];
         // levels with stride >= 64 fold in registers: accumulate slot groups in tree order
         // (per <= 8 keeps the whole lane column in registers; larger P2 folds first)
         uint32_t per_eff = per;
-        double acc_big = 0.0;
-        (void)acc_big;
         if (per <= 8) {
 #pragma unroll
             for (int g = 0; g < 8; ++g) {
                 const uint32_t k = lane + 64u * g;
-                w[g] = (g < (int)per && k < cnt) ? M.at(t + k * step) : 0.0;
+                w[g] = (g < (int)per && k < cnt) ? M.at(t + k * step) : VT(0);
             }
             for (uint32_t s = per >> 1; s >= 1; s >>= 1) {
 #pragma unroll
@@ -205,22 +214,22 @@ __device__ __forceinline__ double dense_window(const Seq& M, uint32_t rule, uint
         } else {
             // large windows: strided partial trees per lane, folded in the same order
             // (position k = lane + 64*g pairs with k + P2/2 = lane + 64*(g + per/2))
-            double col[128];
+            VT col[128];
             for (uint32_t g = 0; g < per_eff; ++g) {
                 const uint32_t k = lane + 64u * g;
-                col[g] = k < cnt ? M.at(t + k * step) : 0.0;
+                col[g] = k < cnt ? M.at(t + k * step) : VT(0);
             }
             for (uint32_t s = per_eff >> 1; s >= 1; s >>= 1)
                 for (uint32_t g = 0; g < s; ++g) col[g] = col[g] + col[g + s];
             w[0] = col[0];
         }
-        double v = w[0];
+        VT v = w[0];
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) {
-            const double u = __shfl_down(v, o, 64);
+            const VT u = __shfl_down(v, o, 64);
             if (lane < (uint32_t)o) v = v + u;
         }
-        res = readlane_f64(v, 0) / (double)cnt;
+        res = readlane_v(v, 0) / (VT)cnt;
     }
     return res;
 }
@@ -246,7 +255,7 @@ __global__ __launch_bounds__(kDenseRecvBlock) void k_dense_recv(const DenseArgs 
             const double lo = S->lo, hi = S->hi;
             const double c = a.byz == 0 ? ((i & 1u) == 0 ? hi + a.delta : lo - a.delta) : a.bconst;
             // blocks (c, nz) and (xi, ns), ordered by value
-            Merged M;
+            Merged<> M;
             M.b = shB;
             const bool cfirst = c <= xi;
             M.v1 = cfirst ? c : xi;
@@ -275,12 +284,23 @@ __global__ __launch_bounds__(kDenseRecvBlock) void k_dense_recv(const DenseArgs 
 // faults: one) and broadcast, instead of once per receiver.  Per round: base multiset -> LDS,
 // bitonic sort (dense_bitonic), ≤ 2 window rules, update, honest (min, max), ε test — no
 // launches, no host round trips (cfg2: ≈ 900 rounds).
+// The rounds' Byzantine class value: SPLIT hi + Δ (class 0) / lo - Δ (class 1), or CONSTANT c;
+// in fp32 mode Δ and c are rounded to binary32 once and the add is binary32 (spec.hpp byz_value_f32).
+__device__ __forceinline__ double dense_byz(const MsgParams& mp, uint32_t w, double lo, double hi, double) {
+    return mp.byz == 0 ? (w == 0 ? hi + mp.delta : lo - mp.delta) : mp.bconst;
+}
+__device__ __forceinline__ float dense_byz(const MsgParams& mp, uint32_t w, double lo, double hi, float) {
+    const float dl = (float)mp.delta;
+    return mp.byz == 0 ? (w == 0 ? (float)hi + dl : (float)lo - dl) : (float)mp.bconst + 0.0f;
+}
+
+template <typename VT = double>
 __global__ __launch_bounds__(kDenseSortBlock) void k_dense_persist(const BatchArgs a, uint32_t kmax) {
-    __shared__ __attribute__((aligned(16))) double xs[kDensePersistMaxN];
-    __shared__ __attribute__((aligned(16))) double sb[kDensePersistMaxN];
+    __shared__ __attribute__((aligned(16))) VT xs[kDensePersistMaxN];
+    __shared__ __attribute__((aligned(16))) VT sb[kDensePersistMaxN];
     __shared__ uint8_t byz[kDensePersistMaxN];   // 1: Byzantine (never updates, never in the base)
     __shared__ uint32_t cnt[4];                  // base size, #Byzantine, #honest-or-active per parity
-    __shared__ double cls[2];
+    __shared__ VT cls[2];
     __shared__ double2 red[kDenseSortBlock / 64];
     const uint32_t lb = blockIdx.x;
     InstState* S = a.st + lb;
@@ -296,7 +316,7 @@ __global__ __launch_bounds__(kDenseSortBlock) void k_dense_persist(const BatchAr
     if (tid < 4) cnt[tid] = 0;
     __syncthreads();
     {
-        const double* xin = ((r & 1u) ? a.x1 : a.x0) + (uint64_t)lb * N;
+        const VT* xin = reinterpret_cast<const VT*>((r & 1u) ? a.x1 : a.x0) + (uint64_t)lb * N;
         uint32_t nz = 0, ne = 0, no = 0;
         for (uint32_t j = tid; j < N; j += kDenseSortBlock) {
             xs[j] = xin[j];
@@ -325,10 +345,10 @@ __global__ __launch_bounds__(kDenseSortBlock) void k_dense_persist(const BatchAr
     bool classed = false;   // every non-Byzantine node holds cls[its class] (after one round here)
     for (uint32_t q = 0; q < kmax && !done; ++q) {
         if (!classed) {   // base multiset B = values of the non-Byzantine senders, sorted
-            for (uint32_t j = tid; j < P; j += kDenseSortBlock) sb[j] = (j < N && !byz[j]) ? xs[j] : kInf;
+            for (uint32_t j = tid; j < P; j += kDenseSortBlock) sb[j] = (j < N && !byz[j]) ? xs[j] : (VT)kInf;
             __syncthreads();
             constexpr int EP = kDensePersistMaxN / kDenseSortBlock;
-            double v[EP];
+            VT v[EP];
             dense_bitonic<EP>(sb, P, v);
             __syncthreads();
 #pragma unroll
@@ -338,28 +358,28 @@ __global__ __launch_bounds__(kDenseSortBlock) void k_dense_persist(const BatchAr
             }
             __syncthreads();
         }
-        double res = 0.0;
+        VT res = VT(0);
         if (w < ncls) {
-            const double c = mp.byz == 0 ? (w == 0 ? hi + mp.delta : lo - mp.delta) : mp.bconst;
+            const VT c = dense_byz(mp, w, lo, hi, VT(0));
             if (!classed) {
-                Merged M;
+                Merged<VT> M;
                 M.b = sb;
                 M.v1 = c;
                 M.n1 = nzv;
                 M.r1 = nzv ? rank_below(sb, nbv, c) : 0;
-                M.v2 = kInf;
+                M.v2 = (VT)kInf;
                 M.n2 = 0;
                 M.r2 = M.r1;
                 res = dense_window(M, a.rule, N, a.trim, lane);
             } else {   // base = {cls0 x n0, cls1 x n1}, plus the Byzantine block {c x nz}
-                double bv[2] = {cls[0], cls[1]};
+                VT bv[2] = {cls[0], cls[1]};
                 uint32_t bn[2] = {ncnt[0], ncnt[1]};
                 if (ncls == 2 && bv[1] < bv[0]) {
-                    const double tv = bv[0]; bv[0] = bv[1]; bv[1] = tv;
+                    const VT tv = bv[0]; bv[0] = bv[1]; bv[1] = tv;
                     const uint32_t tn = bn[0]; bn[0] = bn[1]; bn[1] = tn;
                 }
                 // insert the Byzantine block before the first base run with a value >= c
-                Runs3 R;
+                Runs3<VT> R;
                 if (nzv == 0 || c <= bv[0]) {
                     R.v[0] = c; R.v[1] = bv[0]; R.v[2] = bv[1];
                     R.e[0] = nzv; R.e[1] = nzv + bn[0];
@@ -379,11 +399,11 @@ __global__ __launch_bounds__(kDenseSortBlock) void k_dense_persist(const BatchAr
         double mn = kInf, mx = -kInf;
         for (uint32_t i = tid; i < N; i += kDenseSortBlock) {
             if (byz[i]) continue;   // Byzantine nodes never update
-            const double nv = cls[ncls == 2 ? (i & 1u) : 0u];
+            const VT nv = cls[ncls == 2 ? (i & 1u) : 0u];
             xs[i] = nv;
             if (!stv || stv[i] == kHonest) {
-                mn = __builtin_fmin(mn, nv);
-                mx = __builtin_fmax(mx, nv);
+                mn = __builtin_fmin(mn, (double)nv);
+                mx = __builtin_fmax(mx, (double)nv);
             }
         }
         classed = true;
@@ -401,13 +421,13 @@ __global__ __launch_bounds__(kDenseSortBlock) void k_dense_persist(const BatchAr
         r += 1;
         lo = mn;
         hi = mx;
-        spread = hi - lo;
+        spread = (double)((VT)hi - (VT)lo);   // binary32 subtraction in fp32 mode
         if (a.trace && tid == 0) a.trace[(uint64_t)lb * a.trace_stride + r] = spread;
         conv = spread <= a.eps;
         done = (a.term_eps && conv) || r >= a.max_rounds;
         __syncthreads();   // red is rewritten next round
     }
-    double* xout = ((r & 1u) ? a.x1 : a.x0) + (uint64_t)lb * N;
+    VT* xout = reinterpret_cast<VT*>((r & 1u) ? a.x1 : a.x0) + (uint64_t)lb * N;
     for (uint32_t j = tid; j < N; j += kDenseSortBlock) xout[j] = xs[j];
     if (tid == 0) {
         S->lo = lo;
@@ -422,7 +442,10 @@ __global__ __launch_bounds__(kDenseSortBlock) void k_dense_persist(const BatchAr
 
 hipError_t launch_dense_persist(const BatchArgs& a, uint64_t B, uint32_t k, hipStream_t s) {
     if (a.N > kDensePersistMaxN) return hipErrorNotSupported;
-    hipLaunchKernelGGL(k_dense_persist, dim3((unsigned)B), dim3(kDenseSortBlock), 0, s, a, k);
+    if (a.f32)
+        hipLaunchKernelGGL(k_dense_persist<float>, dim3((unsigned)B), dim3(kDenseSortBlock), 0, s, a, k);
+    else
+        hipLaunchKernelGGL(k_dense_persist<double>, dim3((unsigned)B), dim3(kDenseSortBlock), 0, s, a, k);
     return hipGetLastError();
 }
 

@@ -48,10 +48,17 @@ CASES = {
     "complete_wmsr_split": Config(n_nodes=33, n_instances=8, topology="complete", rule="wmsr", trim=5,
                                   fault_model="byzantine", n_faulty=5, byz_strategy="split", byz_delta=0.2,
                                   eps=1e-6, max_rounds=300, seed=32, trace_spread=True, dtype="f32"),
-    # generic kernel: Byzantine SPLIT trimmed mean on a complete graph (cfg2-like, smaller)
+    # persistent dense kernel: Byzantine SPLIT trimmed mean on a complete graph (cfg2-like, smaller)
     "complete_trimmed_split": Config(n_nodes=256, topology="complete", rule="trimmed", trim=85,
                                      fault_model="byzantine", n_faulty=85, byz_strategy="split",
                                      eps=1e-6, max_rounds=2000, seed=0, trace_spread=True, dtype="f32"),
+    # persistent dense kernel: CONSTANT Byzantine DLPSW, SPLIT midpoint with Δ, several instances
+    "dense_const_dlpsw": Config(n_nodes=300, n_instances=3, topology="complete", rule="dlpsw", trim=40,
+                                fault_model="byzantine", n_faulty=40, byz_strategy="constant", byz_const=-2.5,
+                                eps=1e-6, max_rounds=2000, seed=33, trace_spread=True, dtype="f32"),
+    "dense_split_mid_delta": Config(n_nodes=513, topology="complete", rule="midpoint", trim=100,
+                                    fault_model="byzantine", n_faulty=100, byz_strategy="split", byz_delta=0.01,
+                                    eps=1e-6, max_rounds=2000, seed=34, trace_spread=True, dtype="f32"),
     # odd (d, t): generic kernel on a random-regular graph, DLPSW
     "regular_generic_dlpsw": Config(n_nodes=1000, topology="regular", degree=10, rule="dlpsw", trim=3,
                                     eps=1e-6, max_rounds=300, seed=9, trace_spread=True, dtype="f32"),
@@ -64,7 +71,9 @@ def test_f32_matches_oracle(oracle_mod, name):
     g, o = run_both(oracle_mod, cfg)
     assert g["x"].dtype == np.float32 and o["x"].dtype == np.float32
     assert_same(g, o)
-    assert int(g["rounds"].max()) > (0 if name.startswith("cfg1") else 2)   # cfg1 MIDPOINT converges in 1
+    # cfg1 MIDPOINT, and CONSTANT Byzantine values on a complete graph (every honest receiver holds
+    # the same multiset), agree after one round
+    assert int(g["rounds"].max()) > (0 if name.startswith(("cfg1", "dense_const")) else 1)
 
 
 def test_f32_small_complete_graphs_take_the_batched_kernel():
@@ -72,6 +81,12 @@ def test_f32_small_complete_graphs_take_the_batched_kernel():
         with acsim.Simulator(CASES[name], device=0) as g:
             assert g.kernel_name().startswith("k_batched_small<"), (name, g.kernel_name())
             assert g.kernel_name().endswith("[f32]")
+
+
+def test_f32_complete_graphs_take_the_dense_kernel():
+    for name in ("complete_trimmed_split", "dense_const_dlpsw", "dense_split_mid_delta"):
+        with acsim.Simulator(CASES[name], device=0) as g:
+            assert g.kernel_name() == "k_dense_persist [f32]", (name, g.kernel_name())
 
 
 def test_f32_resume_and_chunks(oracle_mod):
