@@ -107,7 +107,12 @@ def main():
     n = a.n_nodes
     cfg = acsim.preset("cfg4", n_nodes=n, max_rounds=a.warmup + a.steps, instance_offset=rank,
                          dtype=a.dtype)
-    sim = acsim.Simulator(cfg, device=local_rank if world > 1 else 0)
+    dev = 0
+    if world > 1:
+        import torch
+        # device_count() does not initialise the GPU; modulo lets a rehearsal share one card
+        dev = local_rank % max(1, torch.cuda.device_count())
+    sim = acsim.Simulator(cfg, device=dev)
 
     def barrier_sync():
         sim.sync()
