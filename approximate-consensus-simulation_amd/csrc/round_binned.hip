@@ -183,11 +183,14 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
 // ------------------------------------------------------------------------------ phase M
 // mt[g][0..PK] (g = r*K + k): (stage1 start, image offset) of run (a = k*PK + j, r); entry PK holds
 // the image size.  moff[g] .. moff[g+1]: the group's output range in stage2.
-__global__ __launch_bounds__(kBinA) void k_bin_regroup(const double* __restrict__ stage1, const uint2* __restrict__ mt,
+// VT = float for fp32 plans (runs padded to 4 elements, the image holds floats)
+template <typename VT = double>
+__global__ __launch_bounds__(kBinA) void k_bin_regroup(const VT* __restrict__ stage1, const uint2* __restrict__ mt,
                                                      const uint64_t* __restrict__ moff, const uint16_t* __restrict__ idxM,
-                                                     double* __restrict__ stage2, const InstState* __restrict__ st,
+                                                     VT* __restrict__ stage2, const InstState* __restrict__ st,
                                                      uint32_t PK, uint32_t pol) {
-    extern __shared__ double lm[];
+    extern __shared__ __attribute__((aligned(16))) unsigned char lm_raw[];
+    VT* lm = reinterpret_cast<VT*>(lm_raw);
     if (st->done) return;
     const uint32_t g = blockIdx.x;
     constexpr uint32_t NW = kBinA / 64;
@@ -773,7 +776,6 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     G.D = d;
     G.dp = dp;
     G.pad = f32 ? 4u : 2u;
-    if (f32 && levels != 1) return hipErrorNotSupported;   // fp32 plans: one level, clean
     G.SA = sa;
     G.P = (uint32_t)((N + sa - 1) / sa);
     G.Q = (uint32_t)((NR + kBinSB - 1) / kBinSB);
@@ -846,7 +848,7 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
         p.Ep2 = T2.Ep;
         if (e == hipSuccess) e = hipMalloc(&p.idxM, p.Ep2 * 2);
         if (e == hipSuccess) e = hipMemsetAsync(p.idxM, 0, p.Ep2 * 2, s);
-        if (e == hipSuccess) e = hipMalloc(&p.stage2, p.Ep2 * sizeof(double));
+        if (e == hipSuccess) e = hipMalloc(&p.stage2, p.Ep2 * (f32 ? sizeof(float) : sizeof(double)));
         if (e == hipSuccess) e = hipMalloc(&p.moff, ((uint64_t)ng + 1) * sizeof(uint64_t));
         if (e == hipSuccess) {
             hipLaunchKernelGGL(k_bin_fill_m, dim3(grid), dim3(256), 0, s, E, T2.ks, T2.vs, T2.tl, T2.pstart, lpos, p.idxM);
@@ -924,17 +926,26 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
             e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_scatter<float>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 16384 * sizeof(double));
         if (e == hipSuccess)
-            e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_regroup),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, kBinMCap * sizeof(double));
+            e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_regroup<double>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (kBinMCap + 2) * sizeof(double));
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_regroup<float>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (kBinMCap + 4) * sizeof(float));
         if (e != hipSuccess) return e;
         attr = true;
     }
-    if (p.f32) {   // fp32 plans: one level, clean configs
-        if (!clean || p.levels != 1) return hipErrorNotSupported;
+    if (p.f32) {   // fp32 plans: clean configs, one or two levels
+        if (!clean) return hipErrorNotSupported;
         float* st1 = reinterpret_cast<float*>(p.stage1);
         hipLaunchKernelGGL(k_bin_scatter<float>, dim3((p.P + 7) / 8 * 8 * p.segs), dim3(kBinA), p.SA * sizeof(float), s,
                            reinterpret_cast<const float*>(a.xin), p.idxA, p.aoff, st1, a.st, a.N, p.SA, p.segs,
                            p.chunk, pol, fa, fin_on);
+        if (p.levels == 2) {
+            float* st2 = reinterpret_cast<float*>(p.stage2);
+            hipLaunchKernelGGL(k_bin_regroup<float>, dim3(p.ngroups), dim3(kBinA), (p.mcap + 4) * sizeof(float), s, st1,
+                               p.mt, p.moff, p.idxM, st2, a.st, p.PK, pol);
+            st1 = st2;   // phase B reads the regrouped stage
+        }
         const uint32_t nslot = a.nblk > p.Q ? a.nblk : p.Q;
         const uint32_t Qc = (nslot + 7) / 8;
         const dim3 grid(8 * Qc);
@@ -971,7 +982,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
     if (e != hipSuccess) return e;
     const double* last = p.stage1;
     if (p.levels == 2) {
-        hipLaunchKernelGGL(k_bin_regroup, dim3(p.ngroups), dim3(kBinA), (p.mcap + 2) * sizeof(double), s, p.stage1,
+        hipLaunchKernelGGL(k_bin_regroup<double>, dim3(p.ngroups), dim3(kBinA), (p.mcap + 2) * sizeof(double), s, p.stage1,
                            p.mt, p.moff, p.idxM, p.stage2, a.st, p.PK, pol);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         last = p.stage2;

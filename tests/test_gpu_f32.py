@@ -181,3 +181,85 @@ def test_f32_csr_matches_oracle(oracle_mod):
         assert np.array_equal(g.rounds(), o.rounds())
         assert np.array_equal(g.values(0).view(np.uint32), o.values(0).view(np.uint32))
         assert np.array_equal(g.spread_trace(0), o.spread_trace(0))
+
+
+def _with_env(**kw):
+    import contextlib
+    import os
+
+    @contextlib.contextmanager
+    def cm():
+        old = {k: os.environ.get(k) for k in kw}
+        os.environ.update({k: str(v) for k, v in kw.items()})
+        try:
+            yield
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+    return cm()
+
+
+F32_TWO_LEVEL = {
+    # (config, ACSIM_BIN_SA): small source blocks make these graphs two-level plans
+    "d16_t5_n100000_sa256": (Config(n_nodes=100000, topology="regular", degree=16, rule="trimmed", trim=5,
+                                    eps=1e-6, max_rounds=100, seed=21, trace_spread=True, dtype="f32"), 256),
+    "d32_mid_n150001_sa512": (Config(n_nodes=150001, topology="regular", degree=32, rule="midpoint", trim=5,
+                                     eps=1e-6, max_rounds=200, seed=22, trace_spread=True, dtype="f32"), 512),
+    "d8_t2_wmsr_n60001_sa128": (Config(n_nodes=60001, topology="regular", degree=8, rule="wmsr", trim=2,
+                                       eps=1e-6, max_rounds=300, seed=24, trace_spread=True, dtype="f32"), 128),
+}
+
+
+@pytest.mark.parametrize("name", list(F32_TWO_LEVEL))
+def test_f32_two_level_matches_oracle(oracle_mod, name):
+    """fp32 two-level binned plans (float stage1 / phase-M image / stage2, runs padded to 4
+    elements) against the oracle and the fp32 per-lane kernel, bit for bit."""
+    cfg, sa = F32_TWO_LEVEL[name]
+    with _with_env(ACSIM_BIN_SA=sa), acsim.Simulator(cfg, device=0) as g:
+        kb = g.kernel_name()
+        assert "k_bin_regroup" in kb and "f32" in kb, kb
+        g.run()
+        rb, xb, tb = g.rounds(), g.values(0), g.spread_trace(0)
+    with _with_env(ACSIM_BINNED=0), acsim.Simulator(cfg, device=0) as g:
+        assert "k_round_regular" in g.kernel_name()
+        g.run()
+        rl, xl = g.rounds(), g.values(0)
+    with oracle_mod.OracleSimulator(cfg, threads=8) as o:
+        o.run()
+        ro, xo, to = o.rounds(), o.values(0), o.spread_trace(0)
+    assert np.array_equal(rb, ro) and np.array_equal(rl, ro)
+    assert np.array_equal(xb.view(np.uint32), xo.view(np.uint32)), "two-level fp32 values differ from the oracle"
+    assert np.array_equal(xl.view(np.uint32), xo.view(np.uint32))
+    assert np.array_equal(tb, to)
+
+
+@pytest.mark.parametrize("parts", [3])
+def test_f32_two_level_virtual_partitions(oracle_mod, parts):
+    cfg = Config(n_nodes=100000, topology="regular", degree=16, rule="trimmed", trim=5, eps=1e-6,
+                 max_rounds=100, seed=23, dtype="f32")
+    with _with_env(ACSIM_BIN_SA=256), acsim.Simulator(cfg, partitions=parts) as p:
+        assert "k_bin_regroup" in p.kernel_name(), p.kernel_name()
+        p.run()
+        pr, px = p.rounds(), p.values(0)
+    with oracle_mod.OracleSimulator(cfg, threads=8) as o:
+        o.run()
+        assert np.array_equal(o.rounds(), pr)
+        assert np.array_equal(o.values(0).view(np.uint32), px.view(np.uint32))
+
+
+def test_f32_two_level_full_cfg5_matches_per_lane():
+    """Full-size cfg5 graph (N = 2^26, d = 16) in fp32: the two-level plan, 3 FIXED rounds, bit for
+    bit against the fp32 per-lane kernel."""
+    cfg = preset("cfg5", max_rounds=3, trace_spread=True, dtype="f32")
+    with acsim.Simulator(cfg, device=0) as g:
+        kb = g.kernel_name()
+        assert "k_bin_regroup" in kb and "f32" in kb, kb
+        g.run()
+        rb, xb, tb = g.rounds(), g.values(0), g.spread_trace(0)
+    with _with_env(ACSIM_BINNED=0), acsim.Simulator(cfg, device=0) as g:
+        g.run()
+        assert np.array_equal(g.rounds(), rb) and np.array_equal(g.spread_trace(0), tb)
+        assert np.array_equal(g.values(0).view(np.uint32), xb.view(np.uint32))

@@ -25,6 +25,7 @@ CASES = {
     "cfg5": dict(max_rounds=20),
     "cfg4_f32": dict(max_rounds=100),   # fp32 mode
     "cfg3_f32": dict(),
+    "cfg5_f32": dict(max_rounds=20),   # fp32 two-level plan
 }
 
 
