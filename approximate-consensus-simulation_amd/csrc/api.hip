@@ -684,7 +684,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         const char* env = getenv("ACSIM_BINNED");
         const bool allow = !(env && env[0] == '0');
         const uint32_t lv = s->path == PATH_REGULAR && s->d ? binned_levels(s->N, rows_local, s->d, bin_sa, nullptr) : 0;
-        s->binned = allow && (!s->f32 || s->clean) && s->path == PATH_REGULAR && cfg->delay_max == 0 &&
+        s->binned = allow && (!s->f32 || s->clean || s->N <= (1ull << 20)) && s->path == PATH_REGULAR && cfg->delay_max == 0 &&
                     s->B == 1 && lv != 0 &&
                     binned_supported(s->d, cfg->trim, cfg->rule) && rows_local * s->d < (1ull << 32);
         const char* df = getenv("ACSIM_DEFER_FIN");

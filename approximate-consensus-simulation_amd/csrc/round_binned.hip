@@ -207,8 +207,20 @@ __global__ __launch_bounds__(kBinA) void k_bin_regroup(const VT* __restrict__ st
 // 3 silent; bits 2-33 = the sender id (read back for mode 2; B·N < 2^31 with a fault schedule)
 constexpr uint64_t kTagBase = 0x7FF8000000000000ull;
 
-__global__ __launch_bounds__(256) void k_bin_tag(const double* __restrict__ x, const uint32_t* __restrict__ status,
-                                                 double* __restrict__ xt, uint64_t N, uint32_t r,
+// fp32 plans use the binary32 quiet NaN 0x7FC00000 with the same payload layout in
+// its 22 payload bits: bits 0-1 mode, bits 2-21 the sender id (N <= 2^20, checked at create)
+constexpr uint32_t kTagBase32 = 0x7FC00000u;
+
+__device__ __forceinline__ double bin_tag_value(uint64_t j, uint64_t mode, double) {
+    return __longlong_as_double((long long)(kTagBase | j << 2 | mode));
+}
+__device__ __forceinline__ float bin_tag_value(uint64_t j, uint64_t mode, float) {
+    return __uint_as_float(kTagBase32 | (uint32_t)(j << 2 | mode));
+}
+
+template <typename VT = double>
+__global__ __launch_bounds__(256) void k_bin_tag(const VT* __restrict__ x, const uint32_t* __restrict__ status,
+                                                 VT* __restrict__ xt, uint64_t N, uint32_t r,
                                                  const InstState* __restrict__ st) {
     if (st->done) return;
     const uint64_t j = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 2;
@@ -219,7 +231,7 @@ __global__ __launch_bounds__(256) void k_bin_tag(const double* __restrict__ x, c
         if (k >= n) break;
         const uint32_t sj = status[j + k];
         const uint64_t mode = sj == kHonest ? 0 : sj == kByz ? 1 : r < sj ? 0 : r == sj ? 2 : 3;
-        xt[j + k] = mode ? __longlong_as_double((long long)(kTagBase | (j + k) << 2 | mode)) : x[j + k];
+        xt[j + k] = mode ? bin_tag_value(j + k, mode, VT(0)) : x[j + k];
     }
 }
 
@@ -288,7 +300,7 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
                 const MsgParams& mp = a.mp;
                 const uint32_t bI = (uint32_t)mp.inst_offset, bG = bI - bI % mp.mask_group;
                 const uint32_t r = a.r, iu = (uint32_t)i;
-                const double lo = S->lo, hi = S->hi;
+                const VT lo = (VT)S->lo, hi = (VT)S->hi;
 #pragma unroll
                 for (int q = 0; q < D / 4; ++q) {
                     U4 w;
@@ -297,13 +309,22 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const int t = 4 * q + e;
-                        double u = v[1 + t];
-                        const uint64_t bits = (uint64_t)__double_as_longlong(u);
+                        VT u = v[1 + t];
                         uint32_t stj = kHonest;
-                        if ((bits >> 51) == 0xFFFull) {
-                            const uint32_t md = (uint32_t)(bits & 3u);
-                            stj = md == 1 ? kByz : md == 2 ? r : r - 1;   // silent implies r >= 1
-                            if (md == 2) u = a.xin[(bits >> 2) & 0xFFFFFFFFull];
+                        if constexpr (sizeof(VT) == 8) {
+                            const uint64_t bits = (uint64_t)__double_as_longlong(u);
+                            if ((bits >> 51) == 0xFFFull) {
+                                const uint32_t md = (uint32_t)(bits & 3u);
+                                stj = md == 1 ? kByz : md == 2 ? r : r - 1;   // silent implies r >= 1
+                                if (md == 2) u = reinterpret_cast<const VT*>(a.xin)[(bits >> 2) & 0xFFFFFFFFull];
+                            }
+                        } else {
+                            const uint32_t bits = __float_as_uint(u);
+                            if ((bits >> 22) == 0x1FFu) {
+                                const uint32_t md = bits & 3u;
+                                stj = md == 1 ? kByz : md == 2 ? r : r - 1;
+                                if (md == 2) u = reinterpret_cast<const VT*>(a.xin)[(bits >> 2) & 0xFFFFFu];
+                            }
                         }
                         v[1 + t] = resolve_entry(mp, stj, u, xi, w.v[e] < mp.thr, bI, r, iu, (uint64_t)iu * D + t,
                                                  lo, hi);
@@ -934,12 +955,18 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
         if (e != hipSuccess) return e;
         attr = true;
     }
-    if (p.f32) {   // fp32 plans: clean configs, one or two levels
-        if (!clean) return hipErrorNotSupported;
+    if (p.f32) {   // fp32 plans: one or two levels; tagged senders need N <= 2^20
         float* st1 = reinterpret_cast<float*>(p.stage1);
+        const float* fsrc = reinterpret_cast<const float*>(a.xin);
+        if (!clean && a.status) {
+            if (!p.xtag || a.N > (1ull << 20)) return hipErrorInvalidValue;
+            float* xt = reinterpret_cast<float*>(p.xtag);
+            hipLaunchKernelGGL(k_bin_tag<float>, dim3((unsigned)((a.N + 511) / 512)), dim3(256), 0, s, fsrc, a.status,
+                               xt, a.N, a.r, a.st);
+            fsrc = xt;
+        }
         hipLaunchKernelGGL(k_bin_scatter<float>, dim3((p.P + 7) / 8 * 8 * p.segs), dim3(kBinA), p.SA * sizeof(float), s,
-                           reinterpret_cast<const float*>(a.xin), p.idxA, p.aoff, st1, a.st, a.N, p.SA, p.segs,
-                           p.chunk, pol, fa, fin_on);
+                           fsrc, p.idxA, p.aoff, st1, a.st, a.N, p.SA, p.segs, p.chunk, pol, fa, fin_on);
         if (p.levels == 2) {
             float* st2 = reinterpret_cast<float*>(p.stage2);
             hipLaunchKernelGGL(k_bin_regroup<float>, dim3(p.ngroups), dim3(kBinA), (p.mcap + 4) * sizeof(float), s, st1,
@@ -957,6 +984,12 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
         else if (p.ofree)                                                                                \
             hipLaunchKernelGGL((k_bin_gather_of<DD, TT, false, float>), grid, dim3(kBinSB), 0, s, a, st1,   \
                                p.rid, p.rstride, p.tiles, p.nrun, p.Q, Qc);                              \
+        else if (!clean && a.rule == 4)                                                                  \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, true, true, float>), grid, dim3(kBinSB), 0, s, a, st1,  \
+                               p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                      \
+        else if (!clean)                                                                                 \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, false, true, float>), grid, dim3(kBinSB), 0, s, a, st1, \
+                               p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                      \
         else if (a.rule == 4)                                                                            \
             hipLaunchKernelGGL((k_bin_gather<DD, TT, true, false, float>), grid, dim3(kBinSB), 0, s, a, st1, \
                                p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                      \
@@ -972,7 +1005,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
     const double* src = a.xin;
     if (!clean && a.status) {
         if (!p.xtag) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_bin_tag, dim3((unsigned)((a.N + 511) / 512)), dim3(256), 0, s, a.xin, a.status, p.xtag,
+        hipLaunchKernelGGL(k_bin_tag<double>, dim3((unsigned)((a.N + 511) / 512)), dim3(256), 0, s, a.xin, a.status, p.xtag,
                            a.N, a.r, a.st);
         src = p.xtag;
     }

@@ -263,3 +263,66 @@ def test_f32_two_level_full_cfg5_matches_per_lane():
         g.run()
         assert np.array_equal(g.rounds(), rb) and np.array_equal(g.spread_trace(0), tb)
         assert np.array_equal(g.values(0).view(np.uint32), xb.view(np.uint32))
+
+
+F32_TAGGED = {
+    # fault schedules and loss through the fp32 binned exchange (binary32 NaN tags, N <= 2^20)
+    "byzrandom_drop_d32_t5_sa1024": (Config(n_nodes=50000, topology="regular", degree=32, rule="trimmed", trim=5,
+                                            fault_model="byzantine", n_faulty=1500, byz_strategy="random",
+                                            byz_delta=0.2, loss_p=0.1, eps=1e-5, max_rounds=300, seed=42,
+                                            trace_spread=True, dtype="f32"), 1024),
+    "two_level_crash_drop_d16_t5_sa256": (Config(n_nodes=100000, topology="regular", degree=16, rule="trimmed",
+                                                 trim=5, fault_model="crash", n_faulty=3000, crash_window=6,
+                                                 loss_p=0.15, eps=1e-5, max_rounds=300, seed=43, trace_spread=True,
+                                                 dtype="f32"), 256),
+    "avg_drop_d16_sa512": (Config(n_nodes=40000, topology="regular", degree=16, rule="average", loss_p=0.2,
+                                  eps=1e-5, max_rounds=300, seed=44, trace_spread=True, dtype="f32"), 512),
+    "byzconst_mid_d8_sa256": (Config(n_nodes=30001, topology="regular", degree=8, rule="midpoint", trim=2,
+                                     fault_model="byzantine", n_faulty=300, byz_strategy="constant", byz_const=-3.0,
+                                     eps=1e-5, max_rounds=400, seed=45, trace_spread=True, dtype="f32"), 256),
+    "split_dlpsw_d32_sa2048": (Config(n_nodes=40000, topology="regular", degree=32, rule="dlpsw", trim=5,
+                                      fault_model="byzantine", n_faulty=1000, byz_strategy="split", byz_delta=0.1,
+                                      loss_p=0.05, eps=1e-5, max_rounds=300, seed=46, trace_spread=True,
+                                      dtype="f32"), 2048),
+    "wmsr_crash_d16_t5_sa1024": (Config(n_nodes=30000, topology="regular", degree=16, rule="wmsr", trim=5,
+                                        fault_model="crash", n_faulty=600, crash_window=4, loss_p=0.1, eps=1e-5,
+                                        max_rounds=300, seed=47, trace_spread=True, dtype="f32"), 1024),
+}
+
+
+@pytest.mark.parametrize("name", list(F32_TAGGED))
+def test_f32_tagged_binned_matches_oracle(oracle_mod, name):
+    cfg, sa = F32_TAGGED[name]
+    with _with_env(ACSIM_BIN_SA=sa), acsim.Simulator(cfg, device=0) as g:
+        kb = g.kernel_name()
+        assert kb.startswith("k_bin_scatter") and ",faulty>" in kb and "f32" in kb, kb
+        if name.startswith("two_level"):
+            assert "k_bin_regroup" in kb, kb
+        g.run()
+        rb, xb, tb = g.rounds(), g.values(0), g.spread_trace(0)
+    with _with_env(ACSIM_BINNED=0), acsim.Simulator(cfg, device=0) as g:
+        assert "k_round_regular" in g.kernel_name()
+        g.run()
+        rl, xl = g.rounds(), g.values(0)
+    with oracle_mod.OracleSimulator(cfg, threads=8) as o:
+        o.run()
+        ro, xo, to = o.rounds(), o.values(0), o.spread_trace(0)
+    assert np.array_equal(rb, ro) and np.array_equal(rl, ro)
+    assert np.array_equal(xb.view(np.uint32), xo.view(np.uint32)), "tagged fp32 binned values differ from the oracle"
+    assert np.array_equal(xl.view(np.uint32), xo.view(np.uint32))
+    assert np.array_equal(tb, to)
+
+
+def test_f32_tagged_full_cfg4_byz_matches_per_lane():
+    """cfg4_byz at full size (N = 2^20, the largest N the binary32 tag holds) in fp32: 20 FIXED
+    rounds, binned vs per-lane bit for bit."""
+    cfg = preset("cfg4_byz", termination="fixed", max_rounds=20, trace_spread=True, dtype="f32")
+    with acsim.Simulator(cfg, device=0) as g:
+        kb = g.kernel_name()
+        assert ",faulty>" in kb and "f32" in kb, kb
+        g.run()
+        rb, xb, tb = g.rounds(), g.values(0), g.spread_trace(0)
+    with _with_env(ACSIM_BINNED=0), acsim.Simulator(cfg, device=0) as g:
+        g.run()
+        assert np.array_equal(g.rounds(), rb) and np.array_equal(g.spread_trace(0), tb)
+        assert np.array_equal(g.values(0).view(np.uint32), xb.view(np.uint32))

@@ -26,6 +26,7 @@ CASES = {
     "cfg4_f32": dict(max_rounds=100),   # fp32 mode
     "cfg3_f32": dict(),
     "cfg5_f32": dict(max_rounds=20),   # fp32 two-level plan
+    "cfg4_byz_f32": dict(),            # fp32 tagged binned exchange
 }
 
 
