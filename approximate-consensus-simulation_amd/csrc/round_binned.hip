@@ -915,14 +915,18 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     }
     hipError_t e2 = hipStreamSynchronize(s);
     if (e == hipSuccess) e = e2;
-    // phase-A segmentation: about 512 workgroups per launch (two generations per CU measured
-    // faster than one), a multiple of the 4096-position super-step, covering the longest block
+    // phase-A segmentation: about 256 workgroups per launch (one generation: one 128 KiB-LDS
+    // workgroup per CU, each x block staged once per CU; measured 66-68 -> 64 us fp64, 40-42 -> 39.4
+    // us fp32 on cfg4 against 512), a multiple of the 4096-position super-step, covering the
+    // longest block
     if (e == hipSuccess) {
         std::vector<uint64_t> h((uint64_t)G.P + 1);
         e = hipMemcpy(h.data(), p.aoff, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost);
         uint64_t mx = 0;
         for (uint32_t a = 0; a < G.P; ++a) mx = h[a + 1] - h[a] > mx ? h[a + 1] - h[a] : mx;
-        const uint64_t want = (512 + G.P - 1) / G.P;
+        uint64_t awg = 256;   // ACSIM_BIN_AWG: phase-A workgroups per launch (sweeps)
+        if (const char* v = getenv("ACSIM_BIN_AWG")) awg = strtoull(v, nullptr, 10) ? strtoull(v, nullptr, 10) : 256;
+        const uint64_t want = (awg + G.P - 1) / G.P;
         uint64_t ch = (mx + want - 1) / want;
         ch = ch < 8192 ? 8192 : ch;
         p.chunk = (uint32_t)((ch + 4095) / 4096 * 4096);
