@@ -97,7 +97,8 @@ __device__ __forceinline__ void bin_stream(const VT* lx, const uint16_t* __restr
 // Runs are padded to EPU = 16 / sizeof(VT) elements (2 for fp64, 4 for fp32).
 template <typename VT = double>
 __device__ __forceinline__ void bin_dma_runs(const uint2* __restrict__ tb, uint32_t r0, uint32_t r1,
-                                             const VT* __restrict__ src, VT* dst, bool nt = false) {
+                                             const VT* __restrict__ src, VT* dst, bool nt = false,
+                                             uint32_t base = 0) {   // base: image offset of dst[0]
     constexpr uint32_t EPU = 16 / sizeof(VT);
     const uint32_t lane = threadIdx.x & 63;
     const uint4* s16 = reinterpret_cast<const uint4*>(src);
@@ -115,7 +116,7 @@ __device__ __forceinline__ void bin_dma_runs(const uint2* __restrict__ tb, uint3
             const uint32_t pre = __builtin_amdgcn_readlane(dsc.y, k);
             const uint32_t n16 = (__builtin_amdgcn_readlane(nxt, k) - pre) / EPU;   // 16-byte units
             const uint4* sp = s16 + so / EPU + lane;
-            uint4* dp = d16 + pre / EPU;
+            uint4* dp = d16 + (pre - base) / EPU;
             if (nt) {   // once-read runs: nontemporal policy (aux = 2)
                 for (uint32_t o = 0; o < n16; o += 64)
                     if (o + lane < n16) __builtin_amdgcn_global_load_lds(sp + o, dp + o, 16, 0, 2);
@@ -235,14 +236,22 @@ __global__ __launch_bounds__(256) void k_bin_tag(const VT* __restrict__ x, const
     }
 }
 
-template <int D, int T, bool WMSR = false, bool FAULTY = false, typename VT = double>
+// SPLIT (two-pass phase B, ACSIM_BIN_SPLIT): block b's image is copied in two halves (runs
+// [0, nrun/2) then the rest) through an LDS buffer of kBinHalfCap(D) elements; each lane picks up
+// the values of the current half at its invpos positions.  Half the LDS per workgroup: 4 resident
+// workgroups per CU instead of 2.  The plan enables it only when every half fits.
+template <int D, typename VT>
+constexpr uint32_t kBinHalfCap = D * kBinSB / 2 + D * kBinSB / 16;   // + 1/8 for run-length variation and padding
+
+template <int D, int T, bool WMSR = false, bool FAULTY = false, typename VT = double, bool SPLIT = false>
 __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const VT* __restrict__ stage,
                                                        const uint16_t* __restrict__ invpos,
                                                        const uint2* __restrict__ tiles, uint32_t nrun, uint32_t Q,
                                                        uint32_t Qc, uint32_t pol) {
     static_assert(D % 8 == 0, "invpos is read 8 slots at a time");
     // runs are padded to 16-byte multiples; nrun <= D*kBinSB/16 (checked when the plan is built)
-    __shared__ __attribute__((aligned(16))) VT raw[D * kBinSB + D * kBinSB / 16 * (16 / sizeof(VT) - 1)];
+    __shared__ __attribute__((aligned(16)))
+    VT raw[SPLIT ? kBinHalfCap<D, VT> : D * kBinSB + D * kBinSB / 16 * (16 / sizeof(VT) - 1)];
     InstState* S = a.st;
     if (S->done) return;
     // XCD-aware order: consecutive receiver blocks (which share the lines at their tile-run
@@ -277,25 +286,55 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
 #pragma unroll
         for (int q = 0; q < D / 8; ++q) ip[q] = ipp[q * kBinSB];
     }
-    bin_dma_runs(tiles + (uint64_t)b * (nrun + 1), w * nrun / NW, (w + 1) * nrun / NW, stage, raw,
-                 (pol & kPolNtRuns) != 0);
-    __syncthreads();
+    const uint2* tb = tiles + (uint64_t)b * (nrun + 1);
+    VT v[D + 1];
+    if constexpr (!SPLIT) {
+        bin_dma_runs(tb, w * nrun / NW, (w + 1) * nrun / NW, stage, raw, (pol & kPolNtRuns) != 0);
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < D / 8; ++q) {
+            const uint32_t wd[4] = {ip[q].x, ip[q].y, ip[q].z, ip[q].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                v[1 + 8 * q + 2 * e] = raw[wd[e] & 0xFFFFu];
+                v[2 + 8 * q + 2 * e] = raw[wd[e] >> 16];
+            }
+        }
+    } else {
+        const uint32_t js = nrun / 2, nr2 = nrun - js;
+        const uint32_t split = tb[js].y;   // image offset of run js (a multiple of the pad unit)
+        bin_dma_runs(tb, w * js / NW, (w + 1) * js / NW, stage, raw, (pol & kPolNtRuns) != 0);
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < D / 8; ++q) {
+            const uint32_t wd[4] = {ip[q].x, ip[q].y, ip[q].z, ip[q].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t p0 = wd[e] & 0xFFFFu, p1 = wd[e] >> 16;
+                if (p0 < split) v[1 + 8 * q + 2 * e] = raw[p0];
+                if (p1 < split) v[2 + 8 * q + 2 * e] = raw[p1];
+            }
+        }
+        __syncthreads();   // every lane has read the first half before it is overwritten
+        bin_dma_runs(tb, js + w * nr2 / NW, js + (w + 1) * nr2 / NW, stage, raw, (pol & kPolNtRuns) != 0, split);
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < D / 8; ++q) {
+            const uint32_t wd[4] = {ip[q].x, ip[q].y, ip[q].z, ip[q].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t p0 = wd[e] & 0xFFFFu, p1 = wd[e] >> 16;
+                if (p0 >= split) v[1 + 8 * q + 2 * e] = raw[p0 - split];
+                if (p1 >= split) v[2 + 8 * q + 2 * e] = raw[p1 - split];
+            }
+        }
+    }
 
     double mn = kInf, mx = -kInf;
     if (live) {
         VT res = xi;
         if (!FAULTY || is_active(si, a.r)) {
-            VT v[D + 1];
             v[0] = xi;
-#pragma unroll
-            for (int q = 0; q < D / 8; ++q) {
-                const uint32_t wd[4] = {ip[q].x, ip[q].y, ip[q].z, ip[q].w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    v[1 + 8 * q + 2 * e] = raw[wd[e] & 0xFFFFu];
-                    v[2 + 8 * q + 2 * e] = raw[wd[e] >> 16];
-                }
-            }
             if constexpr (FAULTY) {   // §A.5 drops, §A.4 / §A.6 sender resolution (round_regular.hip order)
                 const MsgParams& mp = a.mp;
                 const uint32_t bI = (uint32_t)mp.inst_offset, bG = bI - bI % mp.mask_group;
@@ -915,6 +954,29 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     }
     hipError_t e2 = hipStreamSynchronize(s);
     if (e == hipSuccess) e = e2;
+    // two-pass phase B: on by default where the whole image limits phase B to 2 workgroups per CU
+    // (fp64, d = 32: 68 KiB of LDS; measured 72.7 -> 65.0 us on cfg4; fp32 images already allow 4
+    // and the second pass only costs: 39.3 -> 43.8 us), and only when both halves of every block's
+    // image fit.  ACSIM_BIN_SPLIT=0 / 1 overrides.
+    p.split = false;
+    if (e == hipSuccess && !ofree) {
+        const char* v = getenv("ACSIM_BIN_SPLIT");
+        const bool want = v ? v[0] == '1' : (!f32 && G.D == 32);
+        if (want) {
+            const uint32_t cap = G.D == 32 ? (f32 ? kBinHalfCap<32, float> : kBinHalfCap<32, double>)
+                               : G.D == 16 ? (f32 ? kBinHalfCap<16, float> : kBinHalfCap<16, double>)
+                                           : (f32 ? kBinHalfCap<8, float> : kBinHalfCap<8, double>);
+            std::vector<uint2> h(((uint64_t)p.nrun + 1) * G.Q);
+            e = hipMemcpy(h.data(), p.tiles, h.size() * sizeof(uint2), hipMemcpyDeviceToHost);
+            bool fits = e == hipSuccess;
+            const uint32_t js = p.nrun / 2;
+            for (uint32_t b = 0; fits && b < G.Q; ++b) {
+                const uint32_t sp = h[(uint64_t)b * (p.nrun + 1) + js].y, tot = h[(uint64_t)b * (p.nrun + 1) + p.nrun].y;
+                fits = sp <= cap && tot - sp <= cap;
+            }
+            p.split = fits;
+        }
+    }
     // phase-A segmentation: about 256 workgroups per launch (one generation: one 128 KiB-LDS
     // workgroup per CU, each x block staged once per CU; measured 66-68 -> 64 us fp64, 40-42 -> 39.4
     // us fp32 on cfg4 against 512), a multiple of the 4096-position super-step, covering the
@@ -994,6 +1056,12 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
         else if (!clean)                                                                                 \
             hipLaunchKernelGGL((k_bin_gather<DD, TT, false, true, float>), grid, dim3(kBinSB), 0, s, a, st1, \
                                p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                      \
+        else if (p.split && a.rule == 4)                                                                 \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, true, false, float, true>), grid, dim3(kBinSB), 0, s, a, \
+                               st1, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                 \
+        else if (p.split)                                                                                \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, false, false, float, true>), grid, dim3(kBinSB), 0, s, a, \
+                               st1, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                 \
         else if (a.rule == 4)                                                                            \
             hipLaunchKernelGGL((k_bin_gather<DD, TT, true, false, float>), grid, dim3(kBinSB), 0, s, a, st1, \
                                p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                      \
@@ -1036,6 +1104,12 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
         else if (clean && p.ofree)                                                                       \
             hipLaunchKernelGGL((k_bin_gather_of<DD, TT>), grid, dim3(kBinSB), 0, s, a, last, p.rid,         \
                                p.rstride, p.tiles, p.nrun, p.Q, Qc);                                     \
+        else if (clean && p.split && w_)                                                                 \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, true, false, double, true>), grid, dim3(kBinSB), 0, s, a, \
+                               last, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                \
+        else if (clean && p.split)                                                                       \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, false, false, double, true>), grid, dim3(kBinSB), 0, s, a, \
+                               last, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                \
         else if (clean && w_)                                                                            \
             hipLaunchKernelGGL((k_bin_gather<DD, TT, true>), grid, dim3(kBinSB), 0, s, a, last, p.invpos,   \
                                p.tiles, p.nrun, p.Q, Qc, pol);                                                \

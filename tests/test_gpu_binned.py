@@ -277,3 +277,46 @@ def test_deferred_finalize_matches_standalone(oracle_mod, term):
     for d in (1, 0):
         for got, want in zip(out[d], ref):
             assert np.array_equal(got, want), d
+
+
+SPLIT_CASES = ["d32_t5_eps_n50000_sa1024", "d16_t5_fixed_odd_sa512", "d8_t2_midpoint_sa256",
+               "d32_t5_dlpsw_sa2048", "cfg4_shape_2e17"]
+
+
+@pytest.mark.parametrize("name", SPLIT_CASES)
+def test_split_phase_b_matches_oracle(oracle_mod, name):
+    """Two-pass phase B (ACSIM_BIN_SPLIT=1: half images in LDS) against the oracle, bit for bit."""
+    cfg, sa = CASES[name]
+    if name == "d8_t2_midpoint_sa256":
+        sa = 1024   # a one-level plan (at 256 this graph takes two levels, whose few runs do not halve)
+    with env(ACSIM_BIN_SA=sa, ACSIM_BIN_SPLIT=1):
+        kb, rb, xb, tb = run_gpu(cfg)
+    assert kb.endswith(" split"), kb
+    with oracle_mod.OracleSimulator(cfg, threads=8) as o:
+        o.run()
+        assert np.array_equal(rb, o.rounds()) and np.array_equal(xb, bits(o.values(0)))
+        assert np.array_equal(tb, bits(o.spread_trace(0)))
+
+
+def test_split_phase_b_f32_wmsr_matches_oracle(oracle_mod):
+    cfg = Config(n_nodes=30011, topology="regular", degree=16, rule="wmsr", trim=5, eps=1e-6, max_rounds=300,
+                 seed=31, trace_spread=True, dtype="f32")
+    with env(ACSIM_BIN_SA=512, ACSIM_BIN_SPLIT=1), acsim.Simulator(cfg, device=0) as g:
+        assert g.kernel_name().endswith(" split"), g.kernel_name()
+        g.run()
+        gr, gx = g.rounds(), g.values(0)
+    with oracle_mod.OracleSimulator(cfg, threads=8) as o:
+        o.run()
+        assert np.array_equal(gr, o.rounds())
+        assert np.array_equal(gx.view(np.uint32), o.values(0).view(np.uint32))
+
+
+def test_split_off_matches_oracle(oracle_mod):
+    """ACSIM_BIN_SPLIT=0 keeps the one-pass phase B on a d = 32 fp64 graph (the split default)."""
+    cfg, sa = CASES["cfg4_shape_2e17"]
+    with env(ACSIM_BIN_SA=sa, ACSIM_BIN_SPLIT=0):
+        kb, rb, xb, tb = run_gpu(cfg)
+    assert not kb.endswith(" split"), kb
+    with oracle_mod.OracleSimulator(cfg, threads=8) as o:
+        o.run()
+        assert np.array_equal(rb, o.rounds()) and np.array_equal(xb, bits(o.values(0)))
