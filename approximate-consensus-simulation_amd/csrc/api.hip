@@ -751,7 +751,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         if (s->binned) {   // the plan replaces the ELL in the round loop
             const uint64_t nr = partitioned ? part_rows(s, rank) : s->N;
             if (nr) CREATE_TRY(binned_build(s->bin, s->ell, s->N, nr, s->d, s->dp, bin_sa, tagged, s->f32, bin_of, s->stream));
-            if (s->bin.split && s->clean) s->kname += " split";   // two-pass phase B
+            if (s->bin.split > 1 && s->clean) s->kname += " split" + std::to_string(s->bin.split);   // NP-pass phase B
             (void)hipFree(s->ell);
             s->ell = nullptr;
         }

@@ -126,7 +126,7 @@ struct BinnedPlan {
     uint16_t* invpos = nullptr;         // [Q][D/8][kBinSB][8]: position of (receiver, slot) in block b's runs
     uint2* tiles = nullptr;             // [Q][nrun+1] (stage start | pad count, element offset in block b's runs)
     bool ofree = false;                 // order-free phase B (rid, no invpos)
-    bool split = false;                 // two-pass phase B: half images in LDS (ACSIM_BIN_SPLIT)
+    uint32_t split = 1;                 // phase-B passes over the image (ACSIM_BIN_SPLIT; 1 = whole image)
     uint32_t pol = 0;                   // cache-policy switches (round_binned.hip kPol*)
     uint32_t rstride = 0;               // bytes per receiver block in rid
     uint8_t* rid = nullptr;             // [Q][rstride] receiver inside block b of each image position (ofree)

@@ -236,14 +236,14 @@ __global__ __launch_bounds__(256) void k_bin_tag(const VT* __restrict__ x, const
     }
 }
 
-// SPLIT (two-pass phase B, ACSIM_BIN_SPLIT): block b's image is copied in two halves (runs
-// [0, nrun/2) then the rest) through an LDS buffer of kBinHalfCap(D) elements; each lane picks up
-// the values of the current half at its invpos positions.  Half the LDS per workgroup: 4 resident
-// workgroups per CU instead of 2.  The plan enables it only when every half fits.
-template <int D, typename VT>
-constexpr uint32_t kBinHalfCap = D * kBinSB / 2 + D * kBinSB / 16;   // + 1/8 for run-length variation and padding
+// NP-pass phase B (NP > 1, ACSIM_BIN_SPLIT=NP): block b's image is copied in NP parts (runs
+// [k*nrun/NP, (k+1)*nrun/NP)) through an LDS buffer of kBinPartCap<D, NP> elements; after each
+// part's DMA every lane picks up the values whose invpos falls in that part.  1/NP of the LDS per
+// workgroup: more resident workgroups per CU.  The plan enables it only when every part fits.
+template <int D, int NP>
+constexpr uint32_t kBinPartCap = D * kBinSB / NP + D * kBinSB / 16;   // + 1/16 of the image: run-length variation and padding
 
-template <int D, int T, bool WMSR = false, bool FAULTY = false, typename VT = double, bool SPLIT = false>
+template <int D, int T, bool WMSR = false, bool FAULTY = false, typename VT = double, int NP = 1>
 __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const VT* __restrict__ stage,
                                                        const uint16_t* __restrict__ invpos,
                                                        const uint2* __restrict__ tiles, uint32_t nrun, uint32_t Q,
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
     static_assert(D % 8 == 0, "invpos is read 8 slots at a time");
     // runs are padded to 16-byte multiples; nrun <= D*kBinSB/16 (checked when the plan is built)
     __shared__ __attribute__((aligned(16)))
-    VT raw[SPLIT ? kBinHalfCap<D, VT> : D * kBinSB + D * kBinSB / 16 * (16 / sizeof(VT) - 1)];
+    VT raw[NP > 1 ? kBinPartCap<D, NP> : D * kBinSB + D * kBinSB / 16 * (16 / sizeof(VT) - 1)];
     InstState* S = a.st;
     if (S->done) return;
     // XCD-aware order: consecutive receiver blocks (which share the lines at their tile-run
@@ -288,7 +288,7 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
     }
     const uint2* tb = tiles + (uint64_t)b * (nrun + 1);
     VT v[D + 1];
-    if constexpr (!SPLIT) {
+    if constexpr (NP == 1) {
         bin_dma_runs(tb, w * nrun / NW, (w + 1) * nrun / NW, stage, raw, (pol & kPolNtRuns) != 0);
         __syncthreads();
 #pragma unroll
@@ -301,31 +301,22 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
             }
         }
     } else {
-        const uint32_t js = nrun / 2, nr2 = nrun - js;
-        const uint32_t split = tb[js].y;   // image offset of run js (a multiple of the pad unit)
-        bin_dma_runs(tb, w * js / NW, (w + 1) * js / NW, stage, raw, (pol & kPolNtRuns) != 0);
-        __syncthreads();
+        for (uint32_t k = 0; k < (uint32_t)NP; ++k) {
+            const uint32_t j0 = k * nrun / NP, j1 = (k + 1) * nrun / NP;
+            const uint32_t lo = tb[j0].y, hi = tb[j1].y;   // image range of this part (pad-unit aligned)
+            if (k) __syncthreads();   // every lane has read the previous part before it is overwritten
+            bin_dma_runs(tb, j0 + w * (j1 - j0) / NW, j0 + (w + 1) * (j1 - j0) / NW, stage, raw,
+                         (pol & kPolNtRuns) != 0, lo);
+            __syncthreads();
 #pragma unroll
-        for (int q = 0; q < D / 8; ++q) {
-            const uint32_t wd[4] = {ip[q].x, ip[q].y, ip[q].z, ip[q].w};
+            for (int q = 0; q < D / 8; ++q) {
+                const uint32_t wd[4] = {ip[q].x, ip[q].y, ip[q].z, ip[q].w};
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const uint32_t p0 = wd[e] & 0xFFFFu, p1 = wd[e] >> 16;
-                if (p0 < split) v[1 + 8 * q + 2 * e] = raw[p0];
-                if (p1 < split) v[2 + 8 * q + 2 * e] = raw[p1];
-            }
-        }
-        __syncthreads();   // every lane has read the first half before it is overwritten
-        bin_dma_runs(tb, js + w * nr2 / NW, js + (w + 1) * nr2 / NW, stage, raw, (pol & kPolNtRuns) != 0, split);
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < D / 8; ++q) {
-            const uint32_t wd[4] = {ip[q].x, ip[q].y, ip[q].z, ip[q].w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const uint32_t p0 = wd[e] & 0xFFFFu, p1 = wd[e] >> 16;
-                if (p0 >= split) v[1 + 8 * q + 2 * e] = raw[p0 - split];
-                if (p1 >= split) v[2 + 8 * q + 2 * e] = raw[p1 - split];
+                for (int e = 0; e < 4; ++e) {
+                    const uint32_t p0 = wd[e] & 0xFFFFu, p1 = wd[e] >> 16;
+                    if (p0 >= lo && p0 < hi) v[1 + 8 * q + 2 * e] = raw[p0 - lo];
+                    if (p1 >= lo && p1 < hi) v[2 + 8 * q + 2 * e] = raw[p1 - lo];
+                }
             }
         }
     }
@@ -954,27 +945,27 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     }
     hipError_t e2 = hipStreamSynchronize(s);
     if (e == hipSuccess) e = e2;
-    // two-pass phase B: on by default where the whole image limits phase B to 2 workgroups per CU
-    // (fp64, d = 32: 68 KiB of LDS; measured 72.7 -> 65.0 us on cfg4; fp32 images already allow 4
-    // and the second pass only costs: 39.3 -> 43.8 us), and only when both halves of every block's
-    // image fit.  ACSIM_BIN_SPLIT=0 / 1 overrides.
-    p.split = false;
+    // NP-pass phase B: 2 passes by default where the whole image limits phase B to 2 workgroups
+    // per CU (fp64, d = 32: 68 KiB of LDS; measured 72.7 -> 65.0 us on cfg4; fp32 images already
+    // allow 4 and a second pass only costs: 39.3 -> 43.8 us), and only when every part of every
+    // block's image fits.  ACSIM_BIN_SPLIT=1..4 overrides (1: one pass).
+    p.split = 1;
     if (e == hipSuccess && !ofree) {
         const char* v = getenv("ACSIM_BIN_SPLIT");
-        const bool want = v ? v[0] == '1' : (!f32 && G.D == 32);
-        if (want) {
-            const uint32_t cap = G.D == 32 ? (f32 ? kBinHalfCap<32, float> : kBinHalfCap<32, double>)
-                               : G.D == 16 ? (f32 ? kBinHalfCap<16, float> : kBinHalfCap<16, double>)
-                                           : (f32 ? kBinHalfCap<8, float> : kBinHalfCap<8, double>);
+        uint32_t np = v ? (uint32_t)strtoul(v, nullptr, 10) : (!f32 && G.D == 32 ? 2u : 1u);
+        if (np < 1 || np > 4) np = 1;
+        if (np > 1) {
+            const uint32_t D = G.D;
+            const uint32_t cap = D * kBinSB / np + D * kBinSB / 16;   // kBinPartCap<D, np>
             std::vector<uint2> h(((uint64_t)p.nrun + 1) * G.Q);
             e = hipMemcpy(h.data(), p.tiles, h.size() * sizeof(uint2), hipMemcpyDeviceToHost);
-            bool fits = e == hipSuccess;
-            const uint32_t js = p.nrun / 2;
-            for (uint32_t b = 0; fits && b < G.Q; ++b) {
-                const uint32_t sp = h[(uint64_t)b * (p.nrun + 1) + js].y, tot = h[(uint64_t)b * (p.nrun + 1) + p.nrun].y;
-                fits = sp <= cap && tot - sp <= cap;
-            }
-            p.split = fits;
+            bool fits = e == hipSuccess && p.nrun >= np;
+            for (uint32_t b = 0; fits && b < G.Q; ++b)
+                for (uint32_t k = 0; fits && k < np; ++k) {
+                    const uint2* row = h.data() + (uint64_t)b * (p.nrun + 1);
+                    fits = row[(k + 1) * p.nrun / np].y - row[k * p.nrun / np].y <= cap;
+                }
+            if (fits) p.split = np;
         }
     }
     // phase-A segmentation: about 256 workgroups per launch (one generation: one 128 KiB-LDS
@@ -999,6 +990,20 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     T2.release();
     return e;
 }
+
+// clean phase B in p.split (2..4) passes
+#define ACS_BIN_NP_LAUNCH(DD, TT, W, VT_, SRC)                                                         \
+    {                                                                                                  \
+        if (p.split == 2)                                                                              \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, W, false, VT_, 2>), grid, dim3(kBinSB), 0, s, a, SRC, \
+                               p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                  \
+        else if (p.split == 3)                                                                         \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, W, false, VT_, 3>), grid, dim3(kBinSB), 0, s, a, SRC, \
+                               p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                  \
+        else                                                                                           \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, W, false, VT_, 4>), grid, dim3(kBinSB), 0, s, a, SRC, \
+                               p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                  \
+    }
 
 hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool clean, hipStream_t s,
                                const FinalizeArgs* fin) {
@@ -1056,12 +1061,10 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
         else if (!clean)                                                                                 \
             hipLaunchKernelGGL((k_bin_gather<DD, TT, false, true, float>), grid, dim3(kBinSB), 0, s, a, st1, \
                                p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                      \
-        else if (p.split && a.rule == 4)                                                                 \
-            hipLaunchKernelGGL((k_bin_gather<DD, TT, true, false, float, true>), grid, dim3(kBinSB), 0, s, a, \
-                               st1, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                 \
-        else if (p.split)                                                                                \
-            hipLaunchKernelGGL((k_bin_gather<DD, TT, false, false, float, true>), grid, dim3(kBinSB), 0, s, a, \
-                               st1, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                 \
+        else if (p.split > 1 && a.rule == 4)                                                             \
+            ACS_BIN_NP_LAUNCH(DD, TT, true, float, st1)                                                  \
+        else if (p.split > 1)                                                                            \
+            ACS_BIN_NP_LAUNCH(DD, TT, false, float, st1)                                                 \
         else if (a.rule == 4)                                                                            \
             hipLaunchKernelGGL((k_bin_gather<DD, TT, true, false, float>), grid, dim3(kBinSB), 0, s, a, st1, \
                                p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                      \
@@ -1104,12 +1107,10 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
         else if (clean && p.ofree)                                                                       \
             hipLaunchKernelGGL((k_bin_gather_of<DD, TT>), grid, dim3(kBinSB), 0, s, a, last, p.rid,         \
                                p.rstride, p.tiles, p.nrun, p.Q, Qc);                                     \
-        else if (clean && p.split && w_)                                                                 \
-            hipLaunchKernelGGL((k_bin_gather<DD, TT, true, false, double, true>), grid, dim3(kBinSB), 0, s, a, \
-                               last, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                \
-        else if (clean && p.split)                                                                       \
-            hipLaunchKernelGGL((k_bin_gather<DD, TT, false, false, double, true>), grid, dim3(kBinSB), 0, s, a, \
-                               last, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                \
+        else if (clean && p.split > 1 && w_)                                                             \
+            ACS_BIN_NP_LAUNCH(DD, TT, true, double, last)                                                \
+        else if (clean && p.split > 1)                                                                   \
+            ACS_BIN_NP_LAUNCH(DD, TT, false, double, last)                                               \
         else if (clean && w_)                                                                            \
             hipLaunchKernelGGL((k_bin_gather<DD, TT, true>), grid, dim3(kBinSB), 0, s, a, last, p.invpos,   \
                                p.tiles, p.nrun, p.Q, Qc, pol);                                                \
