@@ -751,7 +751,9 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         if (s->binned) {   // the plan replaces the ELL in the round loop
             const uint64_t nr = partitioned ? part_rows(s, rank) : s->N;
             if (nr) CREATE_TRY(binned_build(s->bin, s->ell, s->N, nr, s->d, s->dp, bin_sa, tagged, s->f32, bin_of, s->stream));
-            if (s->bin.split > 1 && s->clean) s->kname += " split" + std::to_string(s->bin.split);   // NP-pass phase B
+            // NP-pass phase B (slot-dependent configs: fp64, two passes only; see launch_round_binned)
+            if (s->bin.split > 1 && (s->clean || (!s->f32 && s->bin.split == 2)))
+                s->kname += " split" + std::to_string(s->bin.split);
             (void)hipFree(s->ell);
             s->ell = nullptr;
         }

@@ -954,6 +954,8 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
         const char* v = getenv("ACSIM_BIN_SPLIT");
         uint32_t np = v ? (uint32_t)strtoul(v, nullptr, 10) : (!f32 && G.D == 32 ? 2u : 1u);
         if (np < 1 || np > 4) np = 1;
+        if (f32 && tagged && np > 1) np = 1;   // tagged fp32 phase B: one pass (no split instantiation)
+        if (tagged && np > 2) np = 2;          // tagged fp64 phase B: two passes at most
         if (np > 1) {
             const uint32_t D = G.D;
             const uint32_t cap = D * kBinSB / np + D * kBinSB / 16;   // kBinPartCap<D, np>
@@ -1117,6 +1119,12 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
         else if (clean)                                                                                  \
             hipLaunchKernelGGL((k_bin_gather<DD, TT>), grid, dim3(kBinSB), 0, s, a, last, p.invpos, p.tiles, \
                                p.nrun, p.Q, Qc, pol);                                                         \
+        else if (p.split == 2 && w_)   /* faulty: two passes only */                                     \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, true, true, double, 2>), grid, dim3(kBinSB), 0, s, a,  \
+                               last, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                \
+        else if (p.split == 2)                                                                           \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, false, true, double, 2>), grid, dim3(kBinSB), 0, s, a, \
+                               last, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                \
         else if (w_)                                                                                     \
             hipLaunchKernelGGL((k_bin_gather<DD, TT, true, true>), grid, dim3(kBinSB), 0, s, a, last,       \
                                p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                      \

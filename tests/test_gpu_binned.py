@@ -177,7 +177,7 @@ def test_faulty_full_cfg4_byz_matches_per_lane():
     """Full-size cfg4_byz (N = 2^20, 1048 Byzantine RANDOM senders): binned vs per-lane bit for bit."""
     cfg = preset("cfg4_byz", max_rounds=25, trace_spread=True)
     kb, rb, xb, tb = run_gpu(cfg)
-    assert kb.startswith("k_bin_scatter") and kb.endswith("+k_bin_tag"), kb
+    assert kb.startswith("k_bin_scatter") and "+k_bin_tag" in kb, kb
     with env(ACSIM_BINNED=0):
         _, rr, xr, tr = run_gpu(cfg)
     assert np.array_equal(rb, rr) and np.array_equal(xb, xr) and np.array_equal(tb, tr)
@@ -328,6 +328,20 @@ def test_split_more_passes_match_oracle(oracle_mod, np_):
     with env(ACSIM_BIN_SA=sa, ACSIM_BIN_SPLIT=np_):
         kb, rb, xb, tb = run_gpu(cfg)
     assert f" split{np_}" in kb, kb
+    with oracle_mod.OracleSimulator(cfg, threads=8) as o:
+        o.run()
+        assert np.array_equal(rb, o.rounds()) and np.array_equal(xb, bits(o.values(0)))
+        assert np.array_equal(tb, bits(o.spread_trace(0)))
+
+
+@pytest.mark.parametrize("name", ["faulty_d32_t5_byzrandom_drop_sa1024", "faulty_d32_dlpsw_split_sa2048",
+                                  "faulty_cfg4_byz_shape_2e17"])
+def test_split_faulty_matches_oracle(oracle_mod, name):
+    """Two-pass phase B on tagged / lossy fp64 d = 32 plans (the default there) against the oracle."""
+    cfg, sa = CASES[name]
+    with env(ACSIM_BIN_SA=sa):
+        kb, rb, xb, tb = run_gpu(cfg)
+    assert ",faulty>" in kb and " split2" in kb, kb
     with oracle_mod.OracleSimulator(cfg, threads=8) as o:
         o.run()
         assert np.array_equal(rb, o.rounds()) and np.array_equal(xb, bits(o.values(0)))
