@@ -837,7 +837,9 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     G.PK = 1;
     if (levels == 2) {   // chunks of PK source blocks: an LDS image of about 16 Ki deliveries
         const double run1 = (double)NR * d / ((double)G.P * G.R);
-        const uint32_t pk = (uint32_t)(16384.0 / run1);
+        double img = 16384.0;   // ACSIM_BIN_MIMG: target deliveries per phase-M image (sweeps)
+        if (const char* v = getenv("ACSIM_BIN_MIMG")) img = strtod(v, nullptr) > 0 ? strtod(v, nullptr) : img;
+        const uint32_t pk = (uint32_t)(img / run1);
         G.PK = pk < 1 ? 1 : pk > G.P ? G.P : pk;
     }
     G.K = (G.P + G.PK - 1) / G.PK;
@@ -970,7 +972,7 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
             if (fits) p.split = np;
         }
     }
-    // phase-A segmentation: about 256 workgroups per launch (one generation: one 128 KiB-LDS
+    // phase-A segmentation: for few source blocks about 256 workgroups per launch (one generation: one 128 KiB-LDS
     // workgroup per CU, each x block staged once per CU; measured 66-68 -> 64 us fp64, 40-42 -> 39.4
     // us fp32 on cfg4 against 512), a multiple of the 4096-position super-step, covering the
     // longest block
@@ -979,9 +981,16 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
         e = hipMemcpy(h.data(), p.aoff, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost);
         uint64_t mx = 0;
         for (uint32_t a = 0; a < G.P; ++a) mx = h[a + 1] - h[a] > mx ? h[a + 1] - h[a] : mx;
-        uint64_t awg = 256;   // ACSIM_BIN_AWG: phase-A workgroups per launch (sweeps)
-        if (const char* v = getenv("ACSIM_BIN_AWG")) awg = strtoull(v, nullptr, 10) ? strtoull(v, nullptr, 10) : 256;
-        const uint64_t want = (awg + G.P - 1) / G.P;
+        // With more source blocks than CUs (cfg5-sized graphs: several generations anyway), shorter
+        // workgroups of about 48 Ki deliveries measured faster: cfg5 phase A 2525 -> 2085 us at 6
+        // segments per block (profiles/r01_s38_cfg5_awg.txt).
+        uint64_t want = (256 + G.P - 1) / G.P;
+        if (G.P > 256) want = (mx + 49151) / 49152;
+        if (const char* v = getenv("ACSIM_BIN_AWG")) {   // phase-A workgroups per launch (sweeps)
+            const uint64_t awg = strtoull(v, nullptr, 10);
+            if (awg) want = (awg + G.P - 1) / G.P;
+        }
+        if (want == 0) want = 1;
         uint64_t ch = (mx + want - 1) / want;
         ch = ch < 8192 ? 8192 : ch;
         p.chunk = (uint32_t)((ch + 4095) / 4096 * 4096);
