@@ -301,7 +301,8 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
             }
         }
     } else {
-        for (uint32_t k = 0; k < (uint32_t)NP; ++k) {
+#pragma unroll
+        for (uint32_t k = 0; k < (uint32_t)NP; ++k) {   // unrolled: the first / last part skips one bound test
             const uint32_t j0 = k * nrun / NP, j1 = (k + 1) * nrun / NP;
             const uint32_t lo = tb[j0].y, hi = tb[j1].y;   // image range of this part (pad-unit aligned)
             if (k) __syncthreads();   // every lane has read the previous part before it is overwritten
@@ -314,8 +315,8 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const uint32_t p0 = wd[e] & 0xFFFFu, p1 = wd[e] >> 16;
-                    if (p0 >= lo && p0 < hi) v[1 + 8 * q + 2 * e] = raw[p0 - lo];
-                    if (p1 >= lo && p1 < hi) v[2 + 8 * q + 2 * e] = raw[p1 - lo];
+                    if ((k == 0 || p0 >= lo) && (k + 1 == (uint32_t)NP || p0 < hi)) v[1 + 8 * q + 2 * e] = raw[p0 - lo];
+                    if ((k == 0 || p1 >= lo) && (k + 1 == (uint32_t)NP || p1 < hi)) v[2 + 8 * q + 2 * e] = raw[p1 - lo];
                 }
             }
         }
