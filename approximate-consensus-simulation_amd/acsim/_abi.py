@@ -113,6 +113,7 @@ def _declare(lib: C.CDLL) -> None:
         "acs_round": (i32, [vp, u32, P(AcsRoundInfo)]),
         "acs_run": (i32, [vp, P(AcsResult)]),
         "acs_get_values": (i32, [vp, u64, vp, u64]),
+        "acs_get_all_values": (i32, [vp, vp, u64]),
         "acs_get_instance_rounds": (i32, [vp, P(u32), u64]),
         "acs_get_instance_converged": (i32, [vp, P(C.c_uint8), u64]),
         "acs_get_instance_spread": (i32, [vp, P(C.c_double), u64]),
@@ -131,6 +132,10 @@ def _declare(lib: C.CDLL) -> None:
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
+
+
+def library_path() -> str:
+    return LIB_PATH
 
 
 def load_library() -> C.CDLL:

@@ -140,7 +140,10 @@ class Simulator:
         return out
 
     def all_values(self) -> np.ndarray:
-        return np.stack([self.values(b) for b in range(self.B)])
+        """[B, N] values of every instance (one ABI call: acs_get_all_values)."""
+        out = np.empty((self.B, self.N), dtype=self.value_dtype)
+        self._chk(self._lib.acs_get_all_values(self._h, out.ctypes.data, out.size))
+        return out
 
     def rounds(self) -> np.ndarray:
         out = np.empty(self.B, dtype=np.uint32)

@@ -931,6 +931,37 @@ int acs_get_values(acs_sim* s, uint64_t b, void* out, uint64_t n) {
     return ACS_OK;
 }
 
+int acs_get_all_values(acs_sim* s, void* out, uint64_t n) {
+    if (!s || !out || n < s->B * s->N) return fail(ACS_EINVAL, "bad get_all_values arguments");
+    HIP_TRY(hipSetDevice(s->device));
+    std::vector<InstState> v;
+    int rc = read_states(s, v);
+    if (rc) return rc;
+    // instances stop at different rounds: x_b lives in buffer rounds_b % H.  Copy the buffers
+    // holding any instance whole (one transfer each), then pick every instance's row on the host.
+    std::vector<unsigned char> used(s->H, 0);
+    for (const InstState& e : v) used[e.rounds % s->H] = 1;
+    const uint64_t row = s->N * s->es, buf = s->B * s->Npad * s->es;
+    uint32_t only = s->H;
+    for (uint32_t q = 0; q < s->H; ++q)
+        if (used[q]) only = only == s->H ? q : s->H + 1;
+    if (only < s->H && s->Npad == s->N) {   // every instance in one buffer: straight into `out`
+        HIP_TRY(hipMemcpyAsync(out, xb(s, only), s->B * row, hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        return ACS_OK;
+    }
+    std::vector<unsigned char> h((size_t)buf);
+    for (uint32_t q = 0; q < s->H; ++q) {
+        if (!used[q]) continue;
+        HIP_TRY(hipMemcpyAsync(h.data(), xb(s, q), buf, hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        for (uint64_t b = 0; b < s->B; ++b)
+            if (v[b].rounds % s->H == q)
+                memcpy(static_cast<unsigned char*>(out) + b * row, h.data() + b * s->Npad * s->es, row);
+    }
+    return ACS_OK;
+}
+
 int acs_get_partition_values(acs_sim* s, int partition, void* out, uint64_t n) {
     if (!s || !out || n < s->N) return fail(ACS_EINVAL, "bad arguments");
     if (partition < 0 || partition >= (s->virt ? s->nranks : 1)) return fail(ACS_EINVAL, "no such partition copy");
@@ -989,6 +1020,26 @@ int acs_get_spread_trace(acs_sim* s, uint64_t b, double* out, uint64_t n, uint64
 int acs_set_state(acs_sim* s, uint32_t round, const void* x, uint64_t n) {
     if (!s || !x || n != s->B * s->N) return fail(ACS_EINVAL, "set_state needs B*N values");
     if (round > s->c.max_rounds) return fail(ACS_EINVAL, "round > max_rounds");
+    // Values must be finite and bounded (sums of up to kGenericMaxM of them stay finite, so no
+    // NaN can ever appear in x: the tagged binned phase B reads every quiet NaN as a sender tag),
+    // and -0.0 is canonicalised to +0.0 (sorted value sequences stay unique).
+    std::vector<unsigned char> canon(n * s->es);
+    if (s->f32) {
+        const float* xf = static_cast<const float*>(x);
+        float* cf = reinterpret_cast<float*>(canon.data());
+        for (uint64_t k = 0; k < n; ++k) {
+            if (!(fabsf(xf[k]) <= 1e30f)) return fail(ACS_EINVAL, "set_state: value %llu is not finite or |x| > 1e30", (unsigned long long)k);
+            cf[k] = xf[k] + 0.0f;
+        }
+    } else {
+        const double* xd = static_cast<const double*>(x);
+        double* cd = reinterpret_cast<double*>(canon.data());
+        for (uint64_t k = 0; k < n; ++k) {
+            if (!(fabs(xd[k]) <= 1e300)) return fail(ACS_EINVAL, "set_state: value %llu is not finite or |x| > 1e300", (unsigned long long)k);
+            cd[k] = xd[k] + 0.0;
+        }
+    }
+    x = canon.data();
     HIP_TRY(hipSetDevice(s->device));
     for (uint64_t b = 0; b < s->B; ++b) {
         const void* hb = xat(s, x, b * s->N);

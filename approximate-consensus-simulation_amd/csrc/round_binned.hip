@@ -33,6 +33,7 @@
 // written per node per round, against the 8·d B of random gathers the per-lane kernel spends.
 #include <hipcub/hipcub.hpp>
 
+#include <mutex>
 #include <vector>
 
 #include "finalize.hpp"
@@ -302,7 +303,11 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
         }
     } else {
 #pragma unroll
-        for (uint32_t k = 0; k < (uint32_t)NP; ++k) {   // unrolled: the first / last part skips one bound test
+        // Unrolled: the first part skips the p >= lo test and the last part the p < hi test.  This
+        // relies on two invariants of the plan (binned_build checks both on the host): tb[0].y == 0
+        // (lo of part 0), and every lane's invpos — live lanes and the zero-filled padding lanes of
+        // a ragged last block alike — is below tb[nrun].y (hi of the last part).
+        for (uint32_t k = 0; k < (uint32_t)NP; ++k) {
             const uint32_t j0 = k * nrun / NP, j1 = (k + 1) * nrun / NP;
             const uint32_t lo = tb[j0].y, hi = tb[j1].y;   // image range of this part (pad-unit aligned)
             if (k) __syncthreads();   // every lane has read the previous part before it is overwritten
@@ -965,11 +970,14 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
             std::vector<uint2> h(((uint64_t)p.nrun + 1) * G.Q);
             e = hipMemcpy(h.data(), p.tiles, h.size() * sizeof(uint2), hipMemcpyDeviceToHost);
             bool fits = e == hipSuccess && p.nrun >= np;
-            for (uint32_t b = 0; fits && b < G.Q; ++b)
-                for (uint32_t k = 0; fits && k < np; ++k) {
-                    const uint2* row = h.data() + (uint64_t)b * (p.nrun + 1);
+            for (uint32_t b = 0; fits && b < G.Q; ++b) {
+                const uint2* row = h.data() + (uint64_t)b * (p.nrun + 1);
+                // the NP-pass kernel's skipped bound tests: part 0 starts at image offset 0, and the
+                // image is non-empty (padding lanes read invpos 0, which must lie in the last part)
+                fits = row[0].y == 0 && row[p.nrun].y > 0;
+                for (uint32_t k = 0; fits && k < np; ++k)
                     fits = row[(k + 1) * p.nrun / np].y - row[k * p.nrun / np].y <= cap;
-                }
+            }
             if (fits) p.split = np;
         }
     }
@@ -1003,6 +1011,33 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     return e;
 }
 
+// Source blocks above 8192 senders and phase-M images need more than 64 KiB of dynamic LDS.  The
+// attribute belongs to the current device, so it is set once per device ordinal (a process may
+// drive several devices from several threads).
+static hipError_t binned_set_lds_attributes() {
+    constexpr int kMaxDev = 64;
+    static std::once_flag once[kMaxDev];
+    static hipError_t status[kMaxDev];
+    int dev = 0;
+    if (hipError_t e = hipGetDevice(&dev); e != hipSuccess) return e;
+    if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
+    std::call_once(once[dev], [dev] {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_scatter<double>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 16384 * sizeof(double));
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_scatter<float>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 16384 * sizeof(double));
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_regroup<double>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (kBinMCap + 2) * sizeof(double));
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_regroup<float>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (kBinMCap + 4) * sizeof(float));
+        status[dev] = e;
+    });
+    return status[dev];
+}
+
 // clean phase B in p.split (2..4) passes
 #define ACS_BIN_NP_LAUNCH(DD, TT, W, VT_, SRC)                                                         \
     {                                                                                                  \
@@ -1022,22 +1057,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
     const FinalizeArgs fa = fin ? *fin : FinalizeArgs{};
     const uint32_t fin_on = fin ? 1u : 0u;
     const uint32_t pol = p.pol;
-    static bool attr = false;   // source blocks above 8192 senders / phase-M images need > 64 KiB of LDS
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_scatter<double>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 16384 * sizeof(double));
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_scatter<float>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 16384 * sizeof(double));
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_regroup<double>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (kBinMCap + 2) * sizeof(double));
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_regroup<float>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (kBinMCap + 4) * sizeof(float));
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
+    if (hipError_t e = binned_set_lds_attributes(); e != hipSuccess) return e;
     if (p.f32) {   // fp32 plans: one or two levels; tagged senders need N <= 2^20
         float* st1 = reinterpret_cast<float*>(p.stage1);
         const float* fsrc = reinterpret_cast<const float*>(a.xin);

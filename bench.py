@@ -14,19 +14,33 @@ handle's stream over the timed region.  On cfg4 the round is the binned exchange
 (csrc/round_binned.hip): two launches, k_bin_scatter then k_bin_gather, bracketed together by
 one event pair, so "one launch" here means that pair.  The ε-spread fold of the previous round runs
 inside k_bin_scatter (deferred finalize) and is therefore included; the one
-standalone k_finalize per 16-round chunk is not.  Every
---event-every-th timed round (default 10) is bracketed: an event pair idles the stream for
-~5 µs, which would otherwise inflate ms_per_step by ~7 %.
-`traffic` is the pair's measured HBM bytes per round (profiles/pmc_cfg4.json, FETCH_SIZE x 2 +
-WRITE_SIZE, tools/traffic_json.py).  cpu_baseline times the CPU oracle (this
-repo's spec restatement, oracle/) on rank 0 on a bounded sample of the same workload.
+standalone k_finalize per 16-round chunk is not.  Every --event-every-th timed round (default 10)
+is bracketed: an event pair idles the stream for ~5 µs, which would otherwise inflate ms_per_step.
+`traffic` is the pair's measured HBM bytes per round from the committed rocprofv3 PMC summary
+(profiles/pmc_cfg4.json, FETCH_SIZE x 2 + WRITE_SIZE, tools/traffic_json.py); it is reported only
+when that summary was taken on this exact libacsim.so (sha256 match), else null.
+cpu_baseline times the CPU oracle (this repo's spec restatement, oracle/) on rank 0 on a bounded
+sample of the same workload.
+
+Extra legs (every N, each guarded: a failing leg is reported as an error string and never costs
+the headline line; a watchdog prints the line if a leg hangs):
+  cfg3_sharded      10^5 instances x 64 nodes (BASELINE configs[2]) sharded over the ranks by
+                    contiguous global instance blocks, no data-path collective; node-rounds/s
+                    of the whole job, and the checksum of per-instance checksums gathered on
+                    rank 0 compared with tests/golden/fullsize.json.
+  cfg5_partitioned  N = 2^26 random 16-regular (BASELINE configs[4]) node-partitioned over the
+                    ranks with a per-round RCCL all-gather (one plain handle at N = 1); W warm-up
+                    + R timed FIXED rounds, ms/round, the all-gather share, and sha256(x) after
+                    the 10 rounds against the golden hash.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -35,8 +49,12 @@ sys.path.insert(0, PKG)
 
 METRIC = "node-rounds/sec (whole node) + % HBM roofline, trimmed-mean N=1M sparse"
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+FP64_PEAK_TFLOPS = 78.6     # MI355X fp64 vector (= fp64 matrix) peak, vendor datasheet
 BYTES_PER_NODE_ROUND = 400  # 32*4 + 32*8 + 8 + 8
 BYTES_PER_NODE_ROUND_F32 = 264  # SURVEY §8(d) fp32 mode: 32*4 + 32*4 + 4 + 4
+CFG5_BYTES_PER_NODE_ROUND = 208  # 16*4 + 16*8 + 16
+CFG3_FLOP_PER_NODE_ROUND = 128   # 2*64
+GOLDEN = os.path.join(ROOT, "tests", "golden", "fullsize.json")
 
 
 def parse():
@@ -55,6 +73,13 @@ def parse():
     p.add_argument("--event-every", type=int, default=10,
                    help="bracket every k-th timed round with HIP events (each pair idles the "
                         "stream ~5 us, so sampling keeps the timed region representative)")
+    p.add_argument("--legs", default="cfg3,cfg5",
+                   help="comma-separated extra legs (cfg3, cfg5); empty for none")
+    p.add_argument("--leg-timeout", type=float, default=420.0,
+                   help="watchdog: print the line without the unfinished legs after this many seconds")
+    p.add_argument("--allow-shared-device", action="store_true",
+                   help="rehearsal only: run more ranks than GPUs (n_gpus then counts distinct devices "
+                        "and the line is marked shared_device)")
     return p.parse_args()
 
 
@@ -80,16 +105,172 @@ def cpu_baseline(n_nodes: int, seconds: float, dtype: str = "f64") -> dict:
                       f"round, {dt:.1f} s, oracle/acs_oracle.c with {threads} OpenMP threads"}
 
 
+def lib_sha256() -> str:
+    from acsim import _abi
+    path = _abi.library_path()
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 def load_pmc(kernel: str, n_nodes: int, dtype: str = "f64"):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if one matches."""
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if it was taken on this
+    exact build of libacsim.so (same kernel name, size and library sha256); else None."""
     path = os.path.join(ROOT, "profiles", "pmc_cfg4.json" if dtype == "f64" else "pmc_cfg4_f32.json")
     try:
         d = json.load(open(path))
     except Exception:
         return None
-    if d.get("kernel") == kernel and d.get("n_nodes") == n_nodes:
+    if d.get("kernel") == kernel and d.get("n_nodes") == n_nodes and d.get("lib_sha256") == lib_sha256():
         return d.get("hbm_bytes_per_launch")
     return None
+
+
+class Ctx:
+    """Rank / device / collective plumbing shared by the headline and the legs."""
+
+    def __init__(self, world, rank, local_rank, dev, dist):
+        self.world, self.rank, self.local_rank, self.dev, self.dist = world, rank, local_rank, dev, dist
+
+    def barrier(self, sim=None):
+        if sim is not None:
+            sim.sync()
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def max(self, v: float) -> float:
+        if self.dist is None:
+            return float(v)
+        import torch
+        t = torch.tensor([float(v)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def all_ok(self, ok: bool) -> bool:
+        if self.dist is None:
+            return ok
+        import torch
+        t = torch.tensor([1 if ok else 0], dtype=torch.int64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    def gather(self, obj):
+        if self.dist is None:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+
+def golden():
+    try:
+        return json.load(open(GOLDEN))
+    except Exception:
+        return {}
+
+
+def leg_cfg3(ctx: Ctx) -> dict:
+    """BASELINE configs[2]: instance sharding, no data-path collective."""
+    import numpy as np
+    import acsim
+    from acsim.digest import instance_digests, combine_digests
+    from acsim.distributed import shard_range
+    cfg = acsim.preset("cfg3")
+    off, cnt = shard_range(cfg.n_instances, ctx.world, ctx.rank)
+    local = cfg.replace(n_instances=max(cnt, 1), instance_offset=off)
+    sim = None
+    err = None
+    try:
+        with acsim.Simulator(local.replace(n_instances=min(256, max(cnt, 1))), device=ctx.dev) as w:
+            w.run()   # code-object load and first launch outside the timed region
+        sim = acsim.Simulator(local, device=ctx.dev)
+        sim.set_kernel_timing(True)
+    except Exception as e:  # noqa: BLE001
+        err = f"{type(e).__name__}: {e}"
+    if not ctx.all_ok(err is None):
+        raise RuntimeError(err or "another rank failed to create its cfg3 shard")
+    ctx.barrier(sim)
+    t0 = time.perf_counter()
+    sim.run()
+    ctx.barrier(sim)
+    dt = ctx.max(time.perf_counter() - t0)
+    k_ms, k_n, kname = sim.kernel_timing()
+    rounds = sim.rounds()
+    dig = instance_digests(sim.all_values())
+    sim.close()
+    if cnt == 0:
+        rounds, dig = rounds[:0], dig[:0]
+    parts = ctx.gather((off, rounds.astype(np.uint32).tobytes(), dig.tobytes(), k_ms))
+    if ctx.rank != 0:
+        return {}
+    parts.sort(key=lambda p: p[0])
+    all_rounds = np.concatenate([np.frombuffer(p[1], dtype=np.uint32) for p in parts])
+    all_dig = np.concatenate([np.frombuffer(p[2], dtype=np.uint8) for p in parts])
+    node_rounds = int(cfg.n_nodes) * int(all_rounds.astype(np.int64).sum())
+    g = golden().get("cfg3", {})
+    digest = combine_digests(all_dig)
+    kmax = max(p[3] for p in parts) / 1e3
+    flops = CFG3_FLOP_PER_NODE_ROUND * node_rounds
+    return {"workload": "cfg3: 1e5 instances x 64 nodes, complete graph, p=0.2, AVERAGE, eps=1e-6 "
+                        "(SURVEY §A.10), sharded by global instance blocks",
+            "value": node_rounds / dt, "unit": "node-rounds/s", "seconds": dt,
+            "node_rounds": node_rounds, "rounds_max": int(all_rounds.max()),
+            "instances_per_rank": [len(np.frombuffer(p[1], dtype=np.uint32)) for p in parts],
+            "kernel": kname, "kernel_ms_max_rank": kmax * 1e3,
+            "fp64_tflops_kernel": flops / kmax / 1e12 if kmax > 0 else None,
+            "fp64_frac_of_peak": flops / kmax / 1e12 / FP64_PEAK_TFLOPS / ctx.world if kmax > 0 else None,
+            "instances_digest": digest,
+            "golden_match": bool(g) and digest == g.get("instances_digest") and
+                            hashlib.sha256(all_rounds.astype("<u4").tobytes()).hexdigest() == g.get("rounds_sha256")}
+
+
+def leg_cfg5(ctx: Ctx, warm: int = 2, timed: int = 8) -> dict:
+    """BASELINE configs[4]: node partition with a per-round RCCL all-gather."""
+    import acsim
+    from acsim.digest import sha256_values
+    cfg = acsim.preset("cfg5", max_rounds=warm + timed)
+    sim = None
+    err = None
+    try:
+        if ctx.world == 1:
+            sim = acsim.Simulator(cfg, device=ctx.dev)
+        else:
+            from acsim.distributed import partitioned_simulator
+            sim = partitioned_simulator(cfg, ctx.rank, ctx.world, ctx.dev)
+    except Exception as e:  # noqa: BLE001
+        err = f"{type(e).__name__}: {e}"
+    if not ctx.all_ok(err is None):
+        raise RuntimeError(err or "another rank failed to create its cfg5 partition")
+    kname = sim.kernel_name()
+    sim.round(warm)
+    sim.set_kernel_timing(True)
+    ctx.barrier(sim)
+    t0 = time.perf_counter()
+    sim.round(timed)
+    ctx.barrier(sim)
+    dt = ctx.max(time.perf_counter() - t0)
+    k_ms, k_n, _ = sim.kernel_timing()
+    k_ms = ctx.max(k_ms)
+    rounds = int(sim.rounds()[0])
+    out = {}
+    if ctx.rank == 0:
+        x = sim.values(0)
+        h = sha256_values(x)
+        g = golden().get("cfg5", {})
+        n = int(cfg.n_nodes)
+        out = {"workload": f"cfg5: N=2^26 random 16-regular, trimmed t=5, FIXED; {warm} warm-up + "
+                           f"{timed} timed rounds, node-partitioned over {ctx.world} rank(s)"
+                           + (" with a per-round RCCL all-gather" if ctx.world > 1 else ""),
+               "value": n * timed / dt, "unit": "node-rounds/s", "ms_per_round": dt / timed * 1e3,
+               "kernel": kname, "round_kernel_ms_per_round": k_ms / max(1, k_n),
+               "exchange_share": max(0.0, 1.0 - (k_ms / max(1, k_n)) / (dt / timed * 1e3)) if ctx.world > 1 else 0.0,
+               "hbm_frac_unit": CFG5_BYTES_PER_NODE_ROUND * n * timed / dt / 1e9 / (HBM_PEAK_GBS * ctx.world),
+               "rounds": rounds, "x_sha256": h,
+               "golden_match": rounds == 10 and h == g.get("x10_sha256")}
+    sim.close()
+    return out
+
+
+LEGS = {"cfg3": ("cfg3_sharded", leg_cfg3), "cfg5": ("cfg5_partitioned", leg_cfg5)}
 
 
 def main():
@@ -98,63 +279,54 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    ndev = 1
     if world > 1:
         import torch  # imported before libacsim so both share one HIP runtime
         import torch.distributed as dist
         dist.init_process_group("gloo")
+        ndev = max(1, torch.cuda.device_count())   # does not initialise the GPU on this image
+        if world > ndev and not a.allow_shared_device:
+            raise SystemExit(f"{world} ranks but {ndev} GPU(s): one rank per GPU (--allow-shared-device "
+                             f"for a rehearsal that is not a scaling result)")
     import acsim
 
+    dev = local_rank % ndev
+    ctx = Ctx(world, rank, local_rank, dev, dist)
     n = a.n_nodes
     cfg = acsim.preset("cfg4", n_nodes=n, max_rounds=a.warmup + a.steps, instance_offset=rank,
-                         dtype=a.dtype)
-    dev = 0
-    if world > 1:
-        import torch
-        # device_count() does not initialise the GPU; modulo lets a rehearsal share one card
-        dev = local_rank % max(1, torch.cuda.device_count())
+                       dtype=a.dtype)
     sim = acsim.Simulator(cfg, device=dev)
-
-    def barrier_sync():
-        sim.sync()
-        if dist is not None:
-            import torch
-            if torch.cuda.is_available():
-                torch.cuda.synchronize()
-            dist.barrier()
 
     if a.warmup:
         sim.round(a.warmup)
     sim.set_kernel_timing(not a.no_event_timing, every=a.event_every)
-    barrier_sync()
+    ctx.barrier(sim)
     t0 = time.perf_counter()
     sim.round(a.steps)
-    barrier_sync()
+    ctx.barrier(sim)
     dt = time.perf_counter() - t0
     k_ms, k_n, kname = sim.kernel_timing()
     sim.set_kernel_timing(False)
     rounds = int(sim.rounds()[0])
     assert rounds == a.warmup + a.steps, (rounds, a.warmup, a.steps)
-
-    if dist is not None:
-        import torch
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    if rank != 0:
-        sim.close()
-        dist.destroy_process_group()
-        return
+    dt = ctx.max(dt)
+    headline_check = None
+    if rank == 0 and a.dtype == "f64" and n == 1 << 20 and rounds == 100:
+        # the bench workload's own result against the oracle's (tests/golden/fullsize.json)
+        from acsim.digest import sha256_values
+        headline_check = sha256_values(sim.values(0)) == golden().get("cfg4", {}).get("fixed100_x_sha256")
+    sim.close()
 
     value = world * n * a.steps / dt
     avg_launch_s = (k_ms / 1e3 / k_n) if k_n else dt / a.steps
     unit_b = BYTES_PER_NODE_ROUND_F32 if a.dtype == "f32" else BYTES_PER_NODE_ROUND
     achieved = unit_b * n / avg_launch_s / 1e9
-    traffic = load_pmc(kname, n, a.dtype)
+    n_gpus = min(world, ndev)
     out = {
         "metric": METRIC,
         "value": value,
         "unit": "node-rounds/s",
-        "n_gpus": world,
+        "n_gpus": n_gpus,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": dt / a.steps * 1e3,
@@ -168,17 +340,60 @@ def main():
                    "n_nodes": n, "degree": 32, "trim": 5, "instances_per_gpu": 1,
                    "parallelism": "replicas" if world > 1 else "single-gpu"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": kname, "avg_launch_us": avg_launch_s * 1e6,
                      "bytes_per_node_round": unit_b},
-        "hbm_roofline_pct_wall": 100.0 * unit_b * value / world / 1e9 / HBM_PEAK_GBS,
+        "hbm_roofline_pct_wall": 100.0 * unit_b * value / n_gpus / 1e9 / HBM_PEAK_GBS,
+        "cpu_baseline": None,
+        "parity": {"golden_match": headline_check,
+                   "what": "sha256 of rank 0's x after the warm-up + timed rounds (100 in total) equals "
+                           "the oracle's (tests/golden/fullsize.json cfg4.fixed100_x_sha256); null "
+                           "when the run is not that shape"},
     }
-    sim.close()
-    if world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(n, a.cpu_seconds, a.dtype)
-    else:
-        out["cpu_baseline"] = None
-    print(json.dumps(out), flush=True)
+    if world > ndev:
+        out["shared_device"] = True
+        out["ranks"] = world
+    if rank == 0:
+        out["roofline"]["traffic"] = load_pmc(kname, n, a.dtype)
+
+    # --- extra legs, guarded; the watchdog prints the line if one hangs (another rank died in a
+    # collective, a communicator never forms ...)
+    lock = threading.Lock()
+    printed = [False]
+
+    def emit(note=None):
+        with lock:
+            if printed[0] or rank != 0:
+                return
+            if note:
+                out["legs_note"] = note
+            print(json.dumps(out), flush=True)
+            printed[0] = True
+
+    legs = [s for s in a.legs.split(",") if s]
+    if legs:
+        def watchdog():
+            emit(f"watchdog: legs unfinished after {a.leg_timeout:.0f} s")
+            os._exit(0)
+        timer = threading.Timer(a.leg_timeout, watchdog)
+        timer.daemon = True
+        timer.start()
+        for name in legs:
+            key, fn = LEGS[name]
+            try:
+                res = fn(ctx)
+            except Exception as e:  # noqa: BLE001
+                res = {"error": f"{type(e).__name__}: {e}"}
+            if rank == 0:
+                out[key] = res
+        timer.cancel()
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(n, a.cpu_seconds, a.dtype)
+        except Exception as e:  # noqa: BLE001
+            out["cpu_baseline"] = None
+            out["cpu_baseline_error"] = f"{type(e).__name__}: {e}"
+    emit()
     if dist is not None:
         dist.destroy_process_group()
 

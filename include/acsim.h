@@ -178,6 +178,10 @@ int acs_run(struct acs_sim* sim, acs_result* out);
 /* Copy instance's current node values (N values of the config dtype) into a caller buffer. */
 int acs_get_values(struct acs_sim* sim, uint64_t instance, void* out, uint64_t n);
 
+/* Every instance's current values (B*N values, instance-major) in one call; instances that
+ * terminated at different rounds are each read from their own round's buffer. */
+int acs_get_all_values(struct acs_sim* sim, void* out, uint64_t n);
+
 /* Per-instance rounds executed / converged flag / current spread. */
 int acs_get_instance_rounds(struct acs_sim* sim, uint32_t* out, uint64_t n_instances);
 int acs_get_instance_converged(struct acs_sim* sim, uint8_t* out, uint64_t n_instances);

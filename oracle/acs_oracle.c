@@ -643,13 +643,16 @@ int acso_get_spread_trace(acso_sim* s, uint64_t b, double* out, uint64_t n, uint
 int acso_set_state(acso_sim* s, uint32_t round, const double* x, uint64_t n) {
     if (!s || !x || n != s->B * s->N) return fail(ACS_EINVAL, "set_state needs B*N values");
     if (round > s->c.max_rounds) return fail(ACS_EINVAL, "round > max_rounds");
-    if (s->f32)
-        for (uint64_t k = 0; k < n; ++k)
-            if ((double)(float)x[k] != x[k]) return fail(ACS_EINVAL, "fp32 set_state: values must be binary32");
-    memcpy(s->x, x, n * sizeof(double));
+    /* finite and bounded (fp64 |x| <= 1e300, fp32 |x| <= 1e30), -0.0 canonicalised to +0.0:
+     * the same admission rule as the engine's acs_set_state */
+    for (uint64_t k = 0; k < n; ++k) {
+        if (!(fabs(x[k]) <= (s->f32 ? 1e30 : 1e300))) return fail(ACS_EINVAL, "set_state: value not finite or too large");
+        if (s->f32 && (double)(float)x[k] != x[k]) return fail(ACS_EINVAL, "fp32 set_state: values must be binary32");
+    }
+    for (uint64_t k = 0; k < n; ++k) s->x[k] = x[k] + 0.0;
     /* bounded-delay history restarts from x: every past slot holds x^round */
     if (s->hist)
-        for (uint64_t q = 0; q <= s->c.delay_max; ++q) memcpy(s->hist + q * n, x, n * sizeof(double));
+        for (uint64_t q = 0; q <= s->c.delay_max; ++q) memcpy(s->hist + q * n, s->x, n * sizeof(double));
     for (uint64_t b = 0; b < s->B; ++b) {
         s->rounds[b] = round;
         after_update(s, b);

@@ -346,3 +346,35 @@ def test_split_faulty_matches_oracle(oracle_mod, name):
         o.run()
         assert np.array_equal(rb, o.rounds()) and np.array_equal(xb, bits(o.values(0)))
         assert np.array_equal(tb, bits(o.spread_trace(0)))
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_set_state_rejects_nonfinite_on_tagged_plan(oracle_mod, dtype):
+    """a NaN handed to set_state would be read by the tagged phase B as a sender tag
+    (an out-of-range x index).  The ABI rejects NaN / inf / |x| too large and canonicalises -0.0;
+    a crash-fault binned run resumed from a state holding -0.0 still matches the oracle."""
+    cfg = Config(n_nodes=30000, topology="regular", degree=16, rule="trimmed", trim=5, fault_model="crash",
+                 n_faulty=600, crash_window=4, eps=1e-8, max_rounds=300, seed=48, trace_spread=True, dtype=dtype)
+    with env(ACSIM_BIN_SA=1024), acsim.Simulator(cfg, device=0) as g:
+        assert g.kernel_name().startswith("k_bin_scatter") and ",faulty>" in g.kernel_name()
+        g.round(2)
+        x = g.values(0).copy()
+        for bad in (np.nan, np.inf, -np.inf, 1e301 if dtype == "f64" else 2e30):
+            y = x.copy()
+            y[123] = bad
+            with pytest.raises(acsim.AcsError):
+                g.set_state(2, y[None, :])
+        y = x.copy()
+        y[7] = -0.0
+        y[8] = -0.0
+        g.set_state(2, y[None, :])
+        got = g.values(0)
+        assert got[7] == 0 and not np.signbit(got[7])
+        g.run()
+        rg, xg = g.rounds(), g.values(0).copy()
+    with oracle_mod.OracleSimulator(cfg, threads=8) as o:
+        o.set_state(2, y.astype(np.float64)[None, :])
+        o.run()
+        assert np.array_equal(o.rounds(), rg)
+        assert np.array_equal(o.values(0).view(np.uint64 if dtype == "f64" else np.uint32),
+                              xg.view(np.uint64 if dtype == "f64" else np.uint32))

@@ -48,6 +48,8 @@ def test_cfg4_full_size_bit_exact(oracle_mod, name, over):
     kname, gr, gx, gt = run_gpu(cfg)
     assert kname.startswith("k_bin_scatter"), kname   # the headline kernels, not a fallback
     orr, ox, ot = run_oracle(oracle_mod, cfg)
+    if name == "cfg4" and "dtype" not in over:   # the bench workload: also the committed golden hash
+        assert sha256_values(gx) == GOLDEN["cfg4"]["fixed100_x_sha256"]
     assert np.array_equal(gr, orr), (gr, orr)
     assert np.array_equal(bits(gx), bits(ox)), "final values differ"
     assert np.array_equal(bits(gt), bits(ot)), "spread traces differ"
@@ -65,3 +67,95 @@ def test_cfg4_full_size_properties():
     assert x.min() >= x0.min() and x.max() <= x0.max()
     assert np.all(np.diff(tr) <= 0), "spread increased"
     assert tr[-1] < tr[0] * 1e-6
+
+
+# ----------------------------------------------------------------------------- sharded configs
+# BASELINE configs[4] (cfg5) and configs[2] (cfg3) at their full sizes against the golden hashes
+# the oracle wrote (tests/golden/make_golden_fullsize.py; a golden hash match is a bit-for-bit
+# match with the oracle's output).
+import json  # noqa: E402
+
+from acsim.digest import instances_digest, sha256_values  # noqa: E402
+
+GOLDEN = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fullsize.json")))
+
+
+def test_cfg5_full_size_matches_golden():
+    """N = 2^26, random 16-regular, trimmed t = 5 on one GPU (the two-level binned exchange):
+    x after 3 and after 10 FIXED rounds hash to the oracle's, the spread trace matches, and the
+    size-independent properties hold (hull of x^0, spread non-increasing)."""
+    g = GOLDEN["cfg5"]
+    cfg = preset("cfg5", max_rounds=10, trace_spread=True)
+    with acsim.Simulator(cfg, device=0) as s:
+        kname = s.kernel_name()
+        assert kname.startswith("k_bin_scatter+k_bin_regroup"), kname
+        x0 = s.values(0)
+        assert sha256_values(x0) == g["x0_sha256"]
+        lo0, hi0 = float(x0.min()), float(x0.max())
+        del x0
+        s.round(3)
+        x3 = s.values(0)
+        assert sha256_values(x3) == g["x3_sha256"]
+        assert [float(v).hex() for v in x3[:8]] == g["x3_head"]
+        del x3
+        s.round(7)
+        x = s.values(0)
+        assert sha256_values(x) == g["x10_sha256"]
+        tr = s.spread_trace(0)
+    assert [float(v).hex() for v in tr] == g["trace"]
+    assert x.min() >= lo0 and x.max() <= hi0
+    assert np.all(np.diff(tr) <= 0)
+
+
+def test_cfg5_full_size_eight_virtual_partitions():
+    """The 8-GPU data flow of cfg5 (rows split in 8 blocks, each partition reading only its own
+    copy of x, an all-gather after every round) on one device at full size: every private copy
+    hashes to the oracle's x^3."""
+    g = GOLDEN["cfg5"]
+    cfg = preset("cfg5", max_rounds=3)
+    with acsim.Simulator(cfg, device=0, partitions=8) as p:
+        p.run()
+        assert int(p.rounds()[0]) == 3
+        for q in (0, 3, 7):
+            assert sha256_values(p.partition_values(q)) == g["x3_sha256"], f"partition copy {q}"
+
+
+def test_cfg3_full_batch_matches_golden():
+    """10^5 instances x 64 nodes (BASELINE configs[2]) in one handle, and again as 3 instance
+    shards with global instance offsets (the multi-GPU split): both reproduce the oracle's
+    checksum of per-instance checksums and its rounds."""
+    import hashlib
+    from acsim.digest import combine_digests, instance_digests
+    from acsim.distributed import shard_range
+    g = GOLDEN["cfg3"]
+    cfg = preset("cfg3")
+    with acsim.Simulator(cfg, device=0) as s:
+        s.run()
+        x, r = s.all_values(), s.rounds()
+    assert instances_digest(x) == g["instances_digest"]
+    assert hashlib.sha256(r.astype("<u4").tobytes()).hexdigest() == g["rounds_sha256"]
+    digs, rounds = [], []
+    for rank in range(3):
+        off, cnt = shard_range(cfg.n_instances, 3, rank)
+        with acsim.Simulator(cfg.replace(n_instances=cnt, instance_offset=off), device=0) as s:
+            s.run()
+            digs.append(instance_digests(s.all_values()))
+            rounds.append(s.rounds())
+    assert combine_digests(np.concatenate(digs)) == g["instances_digest"]
+    assert np.array_equal(np.concatenate(rounds), r)
+
+
+def test_cfg3_g16_mfma_full_batch_against_oracle(oracle_mod):
+    """The MFMA variant (16-instance groups sharing drop masks) at the full 10^5 instances:
+    rounds identical, values within 1e-12 relative of the oracle (the MFMA accumulation order is
+    the hardware's)."""
+    cfg = preset("cfg3_g16")
+    with acsim.Simulator(cfg, device=0) as s:
+        assert "mfma" in s.kernel_name(), s.kernel_name()
+        s.run()
+        x, r = s.all_values(), s.rounds()
+    with oracle_mod.OracleSimulator(cfg, threads=THREADS) as o:
+        o.run()
+        xo, ro = o.all_values(), o.rounds()
+    assert np.array_equal(r, ro)
+    assert np.max(np.abs(x - xo) / np.abs(xo)) <= 1e-12

@@ -228,3 +228,27 @@ def test_oracle_f32_init_and_resume(oracle_mod):
         b.set_state(4, x4)
         b.run()
         assert b.rounds().tolist() == ra and b.values(0).tobytes() == final
+
+
+def test_oracle_set_state_admission(oracle_mod):
+    """set_state rejects NaN / inf / out-of-range values and canonicalises -0.0: the
+    tagged binned phase B reads any quiet NaN in x as a sender tag, so none may ever enter."""
+    cfg = preset("cfg4_eps", n_nodes=1000)
+    with oracle_mod.OracleSimulator(cfg) as o:
+        x = o.values(0)
+        for bad in (np.nan, np.inf, -np.inf, 1e301):
+            y = x.copy()
+            y[17] = bad
+            with pytest.raises(Exception):
+                o.set_state(2, y)
+        y = x.copy()
+        y[5] = -0.0
+        o.set_state(2, y)
+        got = o.values(0)
+        assert got[5] == 0.0 and not np.signbit(got[5])
+    f = preset("cfg4_eps", n_nodes=1000, dtype="f32")
+    with oracle_mod.OracleSimulator(f) as o:
+        y = o.values(0).astype(np.float64)
+        y[3] = 2e30
+        with pytest.raises(Exception):
+            o.set_state(0, y)

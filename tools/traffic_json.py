@@ -8,7 +8,7 @@ FETCH_SIZE / WRITE_SIZE are KiB per dispatch.  MI355X_MICROARCH.md §HBM: on gfx
 tallies each 128-B read request at 64 B, so it is doubled; WRITE_SIZE is taken as reported.  The
 per-round traffic sums every kernel matching a pattern (the binned round is two launches).
 """
-import collections, csv, glob, json, os, sys
+import collections, csv, glob, hashlib, json, os, sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 d, tag, bench_name, outname, pats = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], sys.argv[5:]
@@ -26,7 +26,9 @@ for k, cs in acc.items():
     per[k] = {"fetch_bytes_corrected": f, "write_bytes": w, "dispatches": len(cs["FETCH_SIZE"])}
     fetch += f
     write += w
+lib = os.path.join(ROOT, "approximate-consensus-simulation_amd", "acsim", "_lib", "libacsim.so")
 rec = {"kernel": bench_name, "n_nodes": 1 << 20, "hbm_bytes_per_launch": fetch + write,
+       "lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),
        "fetch_bytes_corrected": fetch, "write_bytes": write, "per_kernel": per,
        "source": f"profiles/{tag}_pmc.json",
        "correction": "FETCH_SIZE x 2 (MI355X_MICROARCH.md §HBM, gfx950); WRITE_SIZE as reported"}
