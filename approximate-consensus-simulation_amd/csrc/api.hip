@@ -7,6 +7,7 @@
 #include <string.h>
 
 #include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <chrono>
 #include <cstdlib>
@@ -470,6 +471,13 @@ static int flush_finalize(acs_sim* s) {
     return ACS_OK;
 }
 
+// roctx range for the rocprofv3 --marker-trace timeline: host-side enqueue spans of
+// round chunks and persistent launches.
+struct RoctxRange {
+    explicit RoctxRange(const char* m) { roctxRangePushA(m); }
+    ~RoctxRange() { roctxRangePop(); }
+};
+
 // Advance every unfinished instance by at most k rounds.
 static int advance(acs_sim* s, uint32_t k) {
     if (s->all_done || k == 0) return ACS_OK;
@@ -496,6 +504,7 @@ static int advance(acs_sim* s, uint32_t k) {
         hipEvent_t e1;
         int rc = timing_begin(s, &e1);
         if (rc) return rc;
+        RoctxRange range(s->dense_persist ? "acs: persistent dense rounds" : "acs: batched rounds");
         if (s->dense_persist)
             HIP_TRY(launch_dense_persist(a, s->B, k, s->stream));
         else if (s->mfma)
@@ -514,6 +523,7 @@ static int advance(acs_sim* s, uint32_t k) {
     hipEvent_t poll[2] = {nullptr, nullptr};
     while (k > 0 && !s->all_done) {
         const uint32_t chunk = k < kChunk ? k : kChunk;
+        RoctxRange range("acs: round chunk (enqueue)");
         for (uint32_t q = 0; q < chunk; ++q) {
             int rc = enqueue_round(s, s->round + q);
             if (rc) return rc;
@@ -602,6 +612,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(ACS_EDEVICE, "no HIP device");
     if (device < 0 || device >= ndev) return fail(ACS_EINVAL, "device %d out of range", device);
 
+    RoctxRange range("acs: create (graph, plan, fault schedule, x0)");
     acs_sim* s = new acs_sim();
     s->c = *cfg;
     s->device = device;

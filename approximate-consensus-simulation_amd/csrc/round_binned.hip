@@ -48,6 +48,8 @@ constexpr uint32_t kBinMCap = 19456;   // phase-M LDS image capacity (elements, 
 constexpr uint32_t kPolNtRuns = 1;     // phase B: stage runs by nontemporal LDS-DMA
 constexpr uint32_t kPolNtStore = 2;    // phase A / M: nontemporal stage stores
 constexpr uint32_t kPolNtInv = 4;      // phase B: nontemporal invpos loads
+constexpr uint32_t kPolRevB = 8;       // phase B: each XCD walks its receiver-block range downwards
+                                       // (the stage tiles phase A wrote last are read first)
 constexpr uint32_t kPolDefault = kPolNtStore | kPolNtInv;   // measured: phase B 80 -> 71 us, phase A -1 us (cfg4)
 
 // ------------------------------------------------------------------------------ shared pieces
@@ -163,14 +165,15 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
             if (o + threadIdx.x < n16) __builtin_amdgcn_global_load_lds(xs + o, ld + o, 16, 0, 0);
     }
     if (fin_on) {
-        // deferred finalize of the previous round.  Workgroup 0 folds the
+        // deferred finalize of the previous round.  Only workgroup 0 folds the
         // partials and records the verdict (the loads overlap the x staging above; the fold's
-        // barrier drains both).  Under EPS termination every workgroup folds them too and reaches
-        // the same verdict; under FIXED termination the verdict is the round count alone.  A
-        // finished instance stops here.
+        // barrier drains both).  The other workgroups stream unconditionally unless the round
+        // cap is reached: if the EPS test has just ended the run, their stage is never read,
+        // because phase B (the next launch) sees the done flag workgroup 0 set and exits, and
+        // every later launch exits at its first line.  A finished instance stops here.
         bool done;
-        if (fin.term_eps || blockIdx.x == 0) {
-            done = fold_partials<false, kBinA>(fin, 0, blockIdx.x == 0);
+        if (blockIdx.x == 0) {
+            done = fold_partials<false, kBinA>(fin, 0, true);
         } else {
             __syncthreads();
             done = fin.r_next >= fin.max_rounds;
@@ -257,7 +260,7 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
     if (S->done) return;
     // XCD-aware order: consecutive receiver blocks (which share the lines at their tile-run
     // seams) run on the same XCD (dispatch is round-robin over the 8 XCDs by blockIdx)
-    const uint32_t b = (blockIdx.x & 7u) * Qc + (blockIdx.x >> 3);
+    const uint32_t b = (blockIdx.x & 7u) * Qc + ((pol & kPolRevB) ? Qc - 1 - (blockIdx.x >> 3) : (blockIdx.x >> 3));
     if (b >= Q) {   // partial slots past this partition's blocks: neutral (the finalize folds a.nblk)
         if (b < a.nblk && threadIdx.x == 0) a.partial[b] = make_double2(kInf, -kInf);
         return;
@@ -931,7 +934,7 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     p.ofree = ofree;
     {
         const char* v = getenv("ACSIM_BIN_POL");
-        p.pol = v ? (uint32_t)strtoul(v, nullptr, 0) & 7u : kPolDefault;
+        p.pol = v ? (uint32_t)strtoul(v, nullptr, 0) & 15u : kPolDefault;
     }
     if (ofree) {   // order-free phase B: receiver ids in image order
         p.rstride = ((uint32_t)d * kBinSB + p.nrun * (G.pad - 1) + 15u) & ~15u;

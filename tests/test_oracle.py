@@ -7,6 +7,8 @@ import numpy as np
 import pytest
 
 import spec_np as S
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 from acsim.config import Config, preset
 
 GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
@@ -252,3 +254,15 @@ def test_oracle_set_state_admission(oracle_mod):
         y[3] = 2e30
         with pytest.raises(Exception):
             o.set_state(0, y)
+
+
+def test_oracle_under_address_and_ub_sanitizers():
+    """the CPU reference built with -fsanitize=address,undefined runs every config
+    family (complete / regular / CSR, crash / Byzantine / loss / delays, fp32, resume) clean."""
+    import subprocess
+    here = os.path.join(ROOT, "oracle")
+    subprocess.run(["make", "-s", "-C", here, "asan"], check=True)
+    r = subprocess.run([os.path.join(here, "build", "selftest_asan")], capture_output=True, text=True,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1"), timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "selftest ok" in r.stdout

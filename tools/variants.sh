@@ -13,7 +13,7 @@ for v in "$@"; do
   envs=()
   [ "$v" != "-" ] && read -r -a envs <<< "$v"
   env "${envs[@]}" timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/v$n" -o run -- \
-      python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --steps ${STEPS:-50} ${BENCH_EXTRA:-} > "$out/v$n.log" 2>&1
+      python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --legs= --steps ${STEPS:-50} ${BENCH_EXTRA:-} > "$out/v$n.log" 2>&1
   rc=$?
   echo "=== variant $n [$v] rc=$rc"
   [ $rc -ne 0 ] && { tail -5 "$out/v$n.log"; exit $rc; }
