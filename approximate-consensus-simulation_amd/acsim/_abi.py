@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # status codes
 OK, EINVAL, ENOMEM, EDEVICE, ECOMM, EUNSUPPORTED = 0, -1, -2, -3, -4, -5
@@ -25,6 +25,7 @@ FAULT_NONE, FAULT_CRASH, FAULT_BYZANTINE = 0, 1, 2
 BYZ_SPLIT, BYZ_RANDOM, BYZ_CONSTANT = 0, 1, 2
 TERM_EPS, TERM_FIXED = 0, 1
 F64, F32 = 0, 1
+MISSING_SELF, MISSING_OMIT = 0, 1
 
 STREAM_INIT, STREAM_DROP, STREAM_FAULTSET, STREAM_CRASH_ROUND = 0, 1, 2, 3
 STREAM_CRASH_PARTIAL, STREAM_BYZ, STREAM_GRAPH = 4, 5, 6
@@ -60,7 +61,7 @@ class AcsConfig(C.Structure):
         ("omp_threads", C.c_uint32),
         ("instance_offset", C.c_uint64),
         ("delay_max", C.c_uint32),
-        ("reserved0", C.c_uint32),
+        ("missing_policy", C.c_uint32),
     ]
 
 

@@ -23,6 +23,7 @@ _ENUMS = {
     "byz_strategy": {"split": _abi.BYZ_SPLIT, "random": _abi.BYZ_RANDOM,
                      "constant": _abi.BYZ_CONSTANT},
     "termination": {"eps": _abi.TERM_EPS, "fixed": _abi.TERM_FIXED},
+    "missing_policy": {"self": _abi.MISSING_SELF, "omit": _abi.MISSING_OMIT},
     "dtype": {"f64": _abi.F64, "fp64": _abi.F64, "float64": _abi.F64, "f32": _abi.F32,
               "fp32": _abi.F32, "float32": _abi.F32},
 }
@@ -64,6 +65,7 @@ class Config:
     omp_threads: int = 0
     instance_offset: int = 0
     delay_max: int = 0          # bounded-delay rounds; 0 = synchronous
+    missing_policy: object = "self"   # "self" (§A.6 substitution) or "omit" 
 
     def replace(self, **kw) -> "Config":
         return dataclasses.replace(self, **kw)
@@ -100,6 +102,7 @@ class Config:
         c.omp_threads = int(self.omp_threads)
         c.instance_offset = int(self.instance_offset)
         c.delay_max = int(self.delay_max)
+        c.missing_policy = _enum("missing_policy", self.missing_policy)
         return c
 
 

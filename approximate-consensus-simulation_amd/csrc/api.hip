@@ -182,7 +182,7 @@ static int validate(const acs_config* c) {
         !(fabs(c->byz_delta) <= 1e30 && fabs(c->byz_const) <= 1e30))
         return fail(ACS_EINVAL, "fp32: byz_delta / byz_const must satisfy |.| <= 1e30");
     if (c->delay_max > 64) return fail(ACS_EINVAL, "delay_max must be <= 64");
-    if (c->reserved0 != 0) return fail(ACS_EINVAL, "reserved0 must be 0");
+    if (c->missing_policy > ACS_MISSING_OMIT) return fail(ACS_EINVAL, "unknown missing_policy %u", c->missing_policy);
     if (c->trace_spread && c->n_instances * ((uint64_t)c->max_rounds + 1) > (1ull << 28))
         return fail(ACS_EINVAL, "spread trace too large (B*(max_rounds+1) > 2^28)");
     return ACS_OK;
@@ -633,6 +633,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     s->mp.inst_offset = cfg->instance_offset;
     s->mp.delta = cfg->byz_delta;
     s->mp.bconst = cfg->byz_const + 0.0;   // canonicalise -0.0 (no -0 ever enters a sort)
+    s->mp.omit = cfg->missing_policy == ACS_MISSING_OMIT ? 1u : 0u;
     s->nranks = nranks;
     s->partitioned = partitioned;
     s->rank = rank;

@@ -86,7 +86,9 @@ __global__ __launch_bounds__(64) void k_batched_mfma(const BatchArgs a, uint32_t
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
             mrow[m] = miss_s[16 * m + il];
-            wdiag[m] = (double)(1 + __builtin_popcountll(mrow[m]));
+            // §A.6: a missing message is x_i (diagonal weight 1 + #missing); OMIT:
+            // it is left out (weight 1) and the row divides by its present count below
+            wdiag[m] = mp.omit ? 1.0 : (double)(1 + __builtin_popcountll(mrow[m]));
         }
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
@@ -98,7 +100,6 @@ __global__ __launch_bounds__(64) void k_batched_mfma(const BatchArgs a, uint32_t
                 acc[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(w, xb[s], acc[m], 0, 0, 0);
             }
         }
-        __syncthreads();   // miss_s is rewritten next round
         // accumulator (m, reg) holds node 16m + h + 4reg = 4(4m + reg) + h: the B operand of step 4m + reg
         double mn = kInf, mx = -kInf;
 #pragma unroll
@@ -107,7 +108,8 @@ __global__ __launch_bounds__(64) void k_batched_mfma(const BatchArgs a, uint32_t
             for (int g = 0; g < 4; ++g) {
                 const int s = 4 * m + g;
                 const uint32_t node = 4 * s + h;
-                const double v = done ? xb[s] : (node < N ? acc[m][g] / dN : 0.0);
+                const double cnt = mp.omit && node < N ? (double)(N - __builtin_popcountll(miss_s[node])) : dN;
+                const double v = done ? xb[s] : (node < N ? acc[m][g] / cnt : 0.0);
                 xb[s] = v;
                 if (node < N) {
                     mn = __builtin_fmin(mn, v);
@@ -115,6 +117,7 @@ __global__ __launch_bounds__(64) void k_batched_mfma(const BatchArgs a, uint32_t
                 }
             }
         }
+        __syncthreads();   // miss_s is rewritten next round
         // per-instance (column) min / max over the 4 lanes holding its 64 nodes
         mn = __builtin_fmin(mn, __shfl_xor(mn, 16, 64));
         mn = __builtin_fmin(mn, __shfl_xor(mn, 32, 64));

@@ -66,6 +66,7 @@ struct LaneCtx {
     VT xi, lo, hi;
     uint32_t sti;
     uint64_t miss;   // bit j: message from j missing (crash or drop)
+    VT fill;         // missing_policy = OMIT: the value a missing entry takes (omit_fill)
 };
 
 // Byzantine value kept out of line: inlined into each of the P unrolled leaves it multiplied the
@@ -83,7 +84,7 @@ template <bool FAULTS, typename VT>
 __device__ __forceinline__ VT entry_value(const LaneCtx<VT>& c, int j) {
     const VT xj = readlane_v(c.xi, j);
     if ((uint32_t)j == c.lane) return c.xi;
-    if ((c.miss >> j) & 1ull) return c.xi;
+    if ((c.miss >> j) & 1ull) return c.mp->omit ? c.fill : c.xi;   // OMIT: +0.0 / +inf
     if constexpr (FAULTS) {
         const uint32_t stj = (uint32_t)__builtin_amdgcn_readlane((int)c.sti, j);
         if (stj == kByz) return byz_value_ool(*c.mp, c.b, c.r, c.lane, (uint64_t)c.lane * c.N + j, c.lo, c.hi);
@@ -149,9 +150,13 @@ __global__ __launch_bounds__(64) void k_batched_small(const BatchArgs a, uint32_
                     c.miss |= 1ull << j;
             }
         }
+        c.miss &= ~(1ull << lane);   // the self entry is never missing
+        c.fill = omit_fill<VT>(a.rule);
+        // m' = entries present (missing_policy = OMIT); N under §A.6 substitution
+        const uint32_t mn_ = mp.omit ? N - (uint32_t)__builtin_popcountll(c.miss) : N;
         VT res;
         if constexpr (!SORT) {
-            res = average_tree<P, FAULTS>(c, std::make_integer_sequence<int, P>{}) / (VT)N;
+            res = average_tree<P, FAULTS>(c, std::make_integer_sequence<int, P>{}) / (VT)mn_;
         } else {
             VT v[P];
 #pragma unroll
@@ -159,15 +164,17 @@ __global__ __launch_bounds__(64) void k_batched_small(const BatchArgs a, uint32_
             select_sort<P>(v);
 #pragma unroll
             for (int k = 0; k < P; ++k) colbuf[k * 64 + lane] = v[k];
-            const uint32_t t = a.trim, nr = N - 2 * t;
-            if (a.rule == 2) {
-                res = (colbuf[t * 64 + lane] + colbuf[(N - t - 1) * 64 + lane]) * VT(0.5);
+            const uint32_t t = a.trim, nr = mn_ - 2 * t;
+            if (a.rule != 4 && mn_ <= 2 * t) {   // OMIT: too few entries to trim, keep x_i
+                res = xi;
+            } else if (a.rule == 2) {
+                res = (colbuf[t * 64 + lane] + colbuf[(mn_ - t - 1) * 64 + lane]) * VT(0.5);
             } else {
                 uint32_t start = t, step = a.rule == 3 ? t : 1;
                 uint32_t cnt = a.rule == 3 ? (nr + t - 1) / t : nr;
                 if (a.rule == 4) {   // W-MSR: window [min(t, #below), N - min(t, #above))
                     uint32_t nl = 0, ng = 0;
-                    for (uint32_t k = 0; k < N; ++k) {
+                    for (uint32_t k = 0; k < mn_; ++k) {
                         const VT u = colbuf[k * 64 + lane];
                         nl += u < xi;
                         ng += u > xi;
@@ -175,7 +182,7 @@ __global__ __launch_bounds__(64) void k_batched_small(const BatchArgs a, uint32_
                     const uint32_t wlo = nl < t ? nl : t, whi = ng < t ? ng : t;
                     start = wlo;
                     step = 1;
-                    cnt = N - wlo - whi;
+                    cnt = mn_ - wlo - whi;
                 }
                 uint32_t P2 = 1;
                 while (P2 < cnt) P2 <<= 1;

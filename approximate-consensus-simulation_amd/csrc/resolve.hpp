@@ -8,15 +8,32 @@ namespace acs {
 constexpr double kInf = __builtin_huge_val();
 
 // §A.6 resolution of one non-self entry (i <- j, slot s, round r), given the sender's status
-// word, its value x_j, the receiver's x_i and the precomputed §A.5 drop decision.
+// word, its value x_j, the receiver's x_i and the precomputed §A.5 drop decision.  `miss`
+// reports a missing message (x_i is returned for it: the §A.6 self-substitution).
 // VT = double, or float in fp32 mode.
 template <typename VT>
-__device__ __forceinline__ VT resolve_entry(const MsgParams& mp, uint32_t stj, VT xj, VT xi, bool dropped,
-                                            uint32_t b, uint32_t r, uint32_t i, uint64_t s, VT lo, VT hi) {
-    const bool miss = dropped || crash_missing(mp, stj, b, r, s);
+__device__ __forceinline__ VT resolve_entry_m(const MsgParams& mp, uint32_t stj, VT xj, VT xi, bool dropped,
+                                              uint32_t b, uint32_t r, uint32_t i, uint64_t s, VT lo, VT hi,
+                                              bool& miss) {
+    miss = dropped || crash_missing(mp, stj, b, r, s);
     if (miss) return xi;
     if (stj == kByz) return byz_value_t(mp, b, r, i, s, lo, hi);
     return xj;
+}
+
+template <typename VT>
+__device__ __forceinline__ VT resolve_entry(const MsgParams& mp, uint32_t stj, VT xj, VT xi, bool dropped,
+                                            uint32_t b, uint32_t r, uint32_t i, uint64_t s, VT lo, VT hi) {
+    bool miss;
+    return resolve_entry_m(mp, stj, xj, xi, dropped, b, r, i, s, lo, hi, miss);
+}
+
+// The value a missing entry takes under missing_policy = OMIT: +0.0 in AVERAGE's
+// entry-order tree sum (it keeps its place, adds nothing), +inf for the sorting rules (it sorts
+// past every present entry and the rule's window, sized by the present count, excludes it).
+template <typename VT>
+__device__ __forceinline__ VT omit_fill(uint32_t rule) {
+    return rule == 0 ? VT(0) : (VT)__builtin_huge_val();
 }
 
 // DESIGN.md §9 bounded delay: sender j's value as delivered on slot s in round r, given the

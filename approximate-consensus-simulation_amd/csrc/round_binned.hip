@@ -335,6 +335,7 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
         VT res = xi;
         if (!FAULTY || is_active(si, a.r)) {
             v[0] = xi;
+            uint32_t nmiss = 0;   // entries left out under missing_policy = OMIT
             if constexpr (FAULTY) {   // §A.5 drops, §A.4 / §A.6 sender resolution (round_regular.hip order)
                 const MsgParams& mp = a.mp;
                 const uint32_t bI = (uint32_t)mp.inst_offset, bG = bI - bI % mp.mask_group;
@@ -365,12 +366,19 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
                                 if (md == 2) u = reinterpret_cast<const VT*>(a.xin)[(bits >> 2) & 0xFFFFFu];
                             }
                         }
-                        v[1 + t] = resolve_entry(mp, stj, u, xi, w.v[e] < mp.thr, bI, r, iu, (uint64_t)iu * D + t,
-                                                 lo, hi);
+                        bool miss;
+                        const VT rv = resolve_entry_m(mp, stj, u, xi, w.v[e] < mp.thr, bI, r, iu, (uint64_t)iu * D + t,
+                                                      lo, hi, miss);
+                        const bool out = mp.omit && miss;
+                        v[1 + t] = out ? omit_fill<VT>(a.rule) : rv;
+                        nmiss += out;
                     }
                 }
             }
-            res = apply_rule_reg<D, T, WMSR>(a.rule, v);
+            if (FAULTY && a.mp.omit)
+                res = apply_rule_reg_omit<D, T, WMSR>(a.rule, v, nmiss);
+            else
+                res = apply_rule_reg<D, T, WMSR>(a.rule, v);
         }
         reinterpret_cast<VT*>(a.xout)[i] = res;
         if (si == kHonest) {

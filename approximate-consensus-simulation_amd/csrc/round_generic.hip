@@ -5,6 +5,8 @@
 // a power of two with +inf (§A.7; a sort network, so the sorted sequence — and therefore the
 // tree sum — is the spec's), then applies the rule with an LDS stride-halving tree sum.
 // Used for the dense cfg2 shape (N = 1024 complete, t = 341) and any odd (d, t).
+#include <mutex>
+
 #include "resolve.hpp"
 
 namespace acs {
@@ -75,6 +77,10 @@ __global__ __launch_bounds__(kGenericBlock) void k_round_generic(const RoundArgs
     }
     const VT lo = (VT)S->lo, hi = (VT)S->hi;
     const bool avg = a.rule == 0;
+    __shared__ uint32_t nmiss_s;   // entries left out under missing_policy = OMIT
+    if (threadIdx.x == 0) nmiss_s = 0;
+    __syncthreads();
+    uint32_t nmiss = 0;
     for (uint32_t e = threadIdx.x; e < P; e += kGenericBlock) {
         VT v;
         if (e >= m) {
@@ -103,15 +109,24 @@ __global__ __launch_bounds__(kGenericBlock) void k_round_generic(const RoundArgs
                 const uint32_t stj = stv ? stv[j] : kHonest;
                 const bool dropped = mp.thr && draw(mp.key, kStreamDrop, bG, r, slot) < mp.thr;
                 const VT xj = a.delay ? delayed_x<VT>(a, lb, r, draw(mp.key, kStreamDelay, b, r, slot), j) : x[j];
-                v = resolve_entry(mp, stj, xj, xi, dropped, b, r, i, slot, lo, hi);
+                bool miss;
+                v = resolve_entry_m(mp, stj, xj, xi, dropped, b, r, i, slot, lo, hi, miss);
+                if (mp.omit && miss) {
+                    v = omit_fill<VT>(a.rule);
+                    ++nmiss;
+                }
             }
         }
         sh[e] = v;
     }
+    if (nmiss) atomicAdd(&nmiss_s, nmiss);
     __syncthreads();
+    m -= nmiss_s;   // m' = present entries (OMIT); the fillers sort past them (+inf) or add +0.0
     VT res;
     if (avg) {
         res = block_tree_sum(sh, P) / (VT)m;
+    } else if (a.rule != 4 && m <= 2 * a.trim) {   // OMIT: too few entries to trim, keep x_i
+        res = xi;
     } else {
         block_bitonic_sort(sh, P);
         const uint32_t t = a.trim, nr = m - 2 * t;
@@ -157,13 +172,19 @@ hipError_t launch_round_generic(const RoundArgs& a, uint64_t B, hipStream_t s) {
     while (P < a.m) P <<= 1;
     if (P > kGenericMaxM) return hipErrorNotSupported;
     const size_t lds = 2 * (size_t)P * (a.f32 ? sizeof(float) : sizeof(double));
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_round_generic<double>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)(2 * kGenericMaxM * sizeof(double)));
-        if (e != hipSuccess) return e;
-        attr_set = true;
+    {   // > 64 KiB of dynamic LDS: the attribute is per device, set once per device ordinal
+        constexpr int kMaxDev = 64;
+        static std::once_flag once[kMaxDev];
+        static hipError_t status[kMaxDev];
+        int dev = 0;
+        if (hipError_t e = hipGetDevice(&dev); e != hipSuccess) return e;
+        if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
+        std::call_once(once[dev], [dev] {
+            status[dev] = hipFuncSetAttribute((const void*)k_round_generic<double>,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              (int)(2 * kGenericMaxM * sizeof(double)));
+        });
+        if (status[dev] != hipSuccess) return status[dev];
     }
     const dim3 grid((unsigned)a.N, (unsigned)B);
     if (a.f32)

@@ -61,6 +61,7 @@ __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs
             }
             VT v[M];
             v[0] = xi;
+            uint32_t nmiss = 0;   // entries left out under missing_policy = OMIT
             if constexpr (CLEAN) {
 #pragma unroll
                 for (int t = 0; t < D; ++t) v[1 + t] = x[col[t]];
@@ -108,11 +109,18 @@ __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs
                         const int t = 4 * q + e;
                         const uint64_t s = (uint64_t)i * D + t;
                         const bool dropped = w.v[e] < mp.thr;
-                        v[1 + t] = resolve_entry(mp, sj[t], xj[t], xi, dropped, b, r, i, s, lo, hi);
+                        bool miss;
+                        const VT u = resolve_entry_m(mp, sj[t], xj[t], xi, dropped, b, r, i, s, lo, hi, miss);
+                        const bool out = mp.omit && miss;
+                        v[1 + t] = out ? omit_fill<VT>(a.rule) : u;
+                        nmiss += out;
                     }
                 }
             }
-            res = apply_rule_reg<D, T, WMSR>(a.rule, v);
+            if (!CLEAN && a.mp.omit)
+                res = apply_rule_reg_omit<D, T, WMSR>(a.rule, v, nmiss);
+            else
+                res = apply_rule_reg<D, T, WMSR>(a.rule, v);
         }
         xo[i] = res;
         if (honest) {

@@ -147,6 +147,7 @@ struct MsgParams {
     uint64_t inst_offset; // global id of local instance 0
     double delta;         // Δ
     double bconst;        // c
+    uint32_t omit;        // missing_policy = OMIT: missing entries leave S_i
 };
 
 // §A.4 Byzantine value on slot s for receiver i in round r (lo, hi = honest min/max of x^r).

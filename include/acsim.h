@@ -25,7 +25,8 @@
 extern "C" {
 #endif
 
-#define ACS_ABI_VERSION 2   /* 2: acs_config.delay_max (bounded-delay rounds) */
+#define ACS_ABI_VERSION 3   /* 2: acs_config.delay_max (bounded-delay rounds);
+                               3: acs_config.missing_policy (was reserved0), acs_get_all_values */
 
 /* status codes */
 #define ACS_OK            0
@@ -68,6 +69,12 @@ extern "C" {
 /* termination (§A.8) */
 #define ACS_TERM_EPS    0
 #define ACS_TERM_FIXED  1
+
+/* missing-message policy (§A.6): a crashed-silent or dropped message is replaced
+ * by the receiver's own value (SELF, the §A.6 default), or removed from S_i (OMIT: m_i shrinks;
+ * the trimming rules keep x_i when m_i <= 2t) */
+#define ACS_MISSING_SELF 0
+#define ACS_MISSING_OMIT 1
 
 /* value type (§A.0): fp64, or binary32 throughout */
 #define ACS_F64 0
@@ -113,7 +120,7 @@ typedef struct acs_config {
     uint32_t omp_threads;      /* CPU oracle only; ignored by the HIP library */
     uint64_t instance_offset;  /* global id of local instance 0 (multi-GPU instance sharding, §8e) */
     uint32_t delay_max;        /* D: bounded-delay rounds; 0 = synchronous (§A.6) */
-    uint32_t reserved0;        /* must be 0 */
+    uint32_t missing_policy;   /* ACS_MISSING_*: what a missing message becomes */
 } acs_config;
 
 /* Result of acs_round. For B > 1: round = max rounds over instances,

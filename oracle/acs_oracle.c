@@ -191,6 +191,27 @@ static double apply_rule(uint32_t rule, uint32_t t, double* S, uint64_t m, doubl
     return rnd(f32, tree_sum_t(scratch, nq, f32) / (double)nq);
 }
 
+/* DESIGN.md §9, missing_policy = OMIT: the m entries of S in entry order, miss[k] set for the
+ * missing ones (never the self entry), m' = #present >= 1.  AVERAGE: tree_sum over the m entries
+ * in entry order with every missing entry +0.0 (it keeps its place in the tree), divided by m'.
+ * The other rules see only the m' present entries; TRIMMED / MIDPOINT / DLPSW need m' > 2t and
+ * otherwise keep x_i; W-MSR applies as is (its window is never empty). */
+static double apply_rule_omit(uint32_t rule, uint32_t t, double* S, const uint8_t* miss, uint64_t m, double* scratch,
+                              double xi, int f32) {
+    uint64_t mp = 0;
+    if (rule == ACS_RULE_AVERAGE) {
+        for (uint64_t k = 0; k < m; ++k) {
+            if (miss[k]) S[k] = 0.0;
+            else ++mp;
+        }
+        return rnd(f32, tree_sum_t(S, m, f32) / (double)mp);
+    }
+    for (uint64_t k = 0; k < m; ++k)
+        if (!miss[k]) S[mp++] = S[k];
+    if (rule != ACS_RULE_WMSR && mp <= 2ull * t) return xi;
+    return apply_rule(rule, t, S, mp, scratch, xi, f32);
+}
+
 /* ---------------------------------------------------------------- validation (§A.8 constraints) */
 
 int acso_validate(const acs_config* c) {
@@ -262,7 +283,7 @@ int acso_validate(const acs_config* c) {
         !(fabs(c->byz_delta) <= 1e30 && fabs(c->byz_const) <= 1e30))
         return fail(ACS_EINVAL, "fp32: byz_delta / byz_const must satisfy |.| <= 1e30");
     if (c->delay_max > 64) return fail(ACS_EINVAL, "delay_max must be <= 64");
-    if (c->reserved0 != 0) return fail(ACS_EINVAL, "reserved0 must be 0");
+    if (c->missing_policy > ACS_MISSING_OMIT) return fail(ACS_EINVAL, "unknown missing_policy %u", c->missing_policy);
     if (c->trace_spread && c->n_instances * ((uint64_t)c->max_rounds + 1) > (1ull << 28))
         return fail(ACS_EINVAL, "spread trace too large (B*(max_rounds+1) > 2^28)");
     return ACS_OK;
@@ -488,9 +509,12 @@ static double delayed_value(const acso_sim* s, uint64_t lb, uint32_t b, uint32_t
     return s->hist[((uint64_t)((r - delta) % (D + 1)) * s->B + lb) * s->N + j];
 }
 
-/* §A.6: resolve entry (i <- j, slot, round r) for an active receiver i != j-as-self. */
+/* §A.6: resolve entry (i <- j, slot, round r) for an active receiver i != j-as-self.  A missing
+ * entry is x_i under the default policy; under missing_policy = OMIT *miss is set
+ * and the returned value is unused. */
 static double resolve(const acso_sim* s, uint32_t b, uint32_t bG, uint32_t r, const double* x,
-                      const uint32_t* st, uint64_t i, uint64_t j, uint64_t slot, double lo, double hi) {
+                      const uint32_t* st, uint64_t i, uint64_t j, uint64_t slot, double lo, double hi,
+                      int* miss) {
     const uint32_t sj = st[j];
     int missing = 0;
     if (sj != HONEST && sj != BYZ) {           /* crash-faulty sender, crash round sj */
@@ -499,6 +523,7 @@ static double resolve(const acso_sim* s, uint32_t b, uint32_t bG, uint32_t r, co
     }
     if (!missing && s->thr > 0)
         missing = acso_draw(s->c.seed, ACS_STREAM_DROP, bG, r, slot) < s->thr;
+    *miss = missing;
     if (missing) return x[i];
     if (sj == BYZ) return byz_value(s, b, r, i, slot, lo, hi);
     if (s->c.delay_max) return delayed_value(s, (uint64_t)(b - (uint32_t)s->c.instance_offset), b, r, j, slot);
@@ -521,31 +546,46 @@ static void step_instance(acso_sim* s, uint64_t lb) {
     {
         double* S = (double*)malloc(2 * m * sizeof(double));
         double* scratch = S + m;
+        uint8_t* miss = (uint8_t*)malloc(m);
 #pragma omp for schedule(static)
         for (int64_t ii = 0; ii < Ni; ++ii) {
             const uint64_t i = (uint64_t)ii;
             const uint32_t si = st[i];
             const int active = si == HONEST || (si != BYZ && r < si);
             if (!active) { xn[i] = x[i]; continue; }
+            uint64_t mi = m;
             if (c->topology == ACS_TOPO_COMPLETE) {
-                for (uint64_t j = 0; j < N; ++j)
-                    S[j] = j == i ? x[i] : resolve(s, b, bG, r, x, st, i, j, i * N + j, lo, hi);
+                for (uint64_t j = 0; j < N; ++j) {
+                    miss[j] = 0;
+                    int mj = 0;
+                    S[j] = j == i ? x[i] : resolve(s, b, bG, r, x, st, i, j, i * N + j, lo, hi, &mj);
+                    miss[j] = (uint8_t)mj;
+                }
             } else if (c->topology == ACS_TOPO_CSR) {
                 const uint64_t rp = s->rowptr[i], deg = s->rowptr[i + 1] - rp;
                 S[0] = x[i];
-                for (uint64_t t = 0; t < deg; ++t)
-                    S[1 + t] = resolve(s, b, bG, r, x, st, i, s->colidx[rp + t], rp + t, lo, hi);
-                xn[i] = apply_rule(c->rule, c->trim, S, deg + 1, scratch, x[i], s->f32);
-                continue;
+                miss[0] = 0;
+                for (uint64_t t = 0; t < deg; ++t) {
+                    int mj = 0;
+                    S[1 + t] = resolve(s, b, bG, r, x, st, i, s->colidx[rp + t], rp + t, lo, hi, &mj);
+                    miss[1 + t] = (uint8_t)mj;
+                }
+                mi = deg + 1;
             } else {
                 const uint64_t d = c->degree;
                 S[0] = x[i];
-                for (uint64_t t = 0; t < d; ++t)
-                    S[1 + t] = resolve(s, b, bG, r, x, st, i, s->nbr[i * d + t], i * d + t, lo, hi);
+                miss[0] = 0;
+                for (uint64_t t = 0; t < d; ++t) {
+                    int mj = 0;
+                    S[1 + t] = resolve(s, b, bG, r, x, st, i, s->nbr[i * d + t], i * d + t, lo, hi, &mj);
+                    miss[1 + t] = (uint8_t)mj;
+                }
             }
-            xn[i] = apply_rule(c->rule, c->trim, S, m, scratch, x[i], s->f32);
+            xn[i] = c->missing_policy == ACS_MISSING_OMIT ? apply_rule_omit(c->rule, c->trim, S, miss, mi, scratch, x[i], s->f32)
+                                                         : apply_rule(c->rule, c->trim, S, mi, scratch, x[i], s->f32);
         }
         free(S);
+        free(miss);
     }
     /* swap x / xn for this instance; keep x^{r+1} in the delay history */
     memcpy(s->x + lb * N, xn, N * sizeof(double));

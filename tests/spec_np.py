@@ -137,6 +137,43 @@ def apply_rule(rule: int, t: int, S: np.ndarray, xi=None) -> np.ndarray:
     return tree_sum_rows(Q) / ft(Q.shape[1])
 
 
+def apply_rule_omit(rule: int, t: int, S: np.ndarray, miss: np.ndarray, xi) -> np.ndarray:
+    """DESIGN.md §9 missing_policy = OMIT, rows of S with a missing-entry mask (self never
+    missing): AVERAGE sums the entry-order row with +0.0 in the missing places and divides by
+    m' = #present; the other rules see only the present entries, and TRIMMED / MIDPOINT / DLPSW
+    keep x_i when m' <= 2t.  Written with +inf fillers (they sort last) and masked windows
+    (zero padding past a window leaves the stride-halving sum unchanged)."""
+    ft = S.dtype.type
+    m = S.shape[1]
+    mp = m - miss.sum(axis=1)
+    xi = np.asarray(xi, dtype=S.dtype)
+    if rule == 0:
+        return tree_sum_rows(np.where(miss, ft(0), S)) / mp.astype(S.dtype)
+    Ss = np.sort(np.where(miss, ft(np.inf), S), axis=1)
+    k = np.arange(m)[None, :]
+    if rule == 4:
+        lo = np.minimum(t, (Ss < xi[:, None]).sum(axis=1))
+        hi = np.minimum(t, (Ss > xi[:, None]).sum(axis=1) - miss.sum(axis=1))
+        nw = mp - lo - hi
+        idx = np.minimum(lo[:, None] + k, m - 1)
+        W = np.where(k < nw[:, None], np.take_along_axis(Ss, idx, axis=1), ft(0))
+        return tree_sum_rows(W) / nw.astype(S.dtype)
+    ok = mp > 2 * t
+    nr = np.where(ok, mp - 2 * t, 1)
+    rows = np.arange(S.shape[0])
+    if rule == 2:
+        res = (Ss[:, t] + Ss[rows, np.where(ok, mp - t - 1, t)]) * ft(0.5)
+    else:
+        step = t if rule == 3 else 1
+        cnt = (nr + step - 1) // step
+        width = (m - 2 * t + step - 1) // step
+        kk = np.arange(width)[None, :]
+        idx = np.minimum(t + kk * step, m - 1)
+        W = np.where(kk < cnt[:, None], np.take_along_axis(Ss, np.broadcast_to(idx, (S.shape[0], width)), axis=1), ft(0))
+        res = tree_sum_rows(W) / cnt.astype(S.dtype)
+    return np.where(ok, res, xi)
+
+
 class NpSim:
     """Vectorised restatement of one configuration (attribute names as acsim.Config)."""
 
@@ -189,6 +226,7 @@ class NpSim:
         self.rounds = np.zeros(self.B, dtype=np.int64)
         # bounded-delay rounds: every past x^q, q = 0..r
         self.D = int(getattr(cfg, "delay_max", 0))
+        self.omit = _enum("missing_policy", getattr(cfg, "missing_policy", "self")) == 1
         self.hist = [[self.x[lb].copy()] for lb in range(self.B)]
         self.trace = [[] for _ in range(self.B)]
         self.lo = np.zeros(self.B, dtype=self.ft)
@@ -229,8 +267,8 @@ class NpSim:
                 slots = np.concatenate([[0], np.arange(rp, re_)]).astype(np.uint64)[None, :]
                 selfm = np.zeros(J.shape, dtype=bool)
                 selfm[0, 0] = True
-                V = self._values(np.array([i]), J, slots, selfm, r, b, bG, x, st, lo, hi)
-                xn[i] = apply_rule(self.rule, self.t, V, x[[i]])[0]
+                V, miss = self._values(np.array([i]), J, slots, selfm, r, b, bG, x, st, lo, hi)
+                xn[i] = self._rule(V, miss, x[[i]])[0]
         elif A.size:
             if self.topo == 0:
                 J = np.broadcast_to(np.arange(N), (A.size, N))
@@ -244,12 +282,17 @@ class NpSim:
                      A[:, None].astype(np.uint64) * np.uint64(self.d) + tt[None, :]], axis=1)
                 selfm = np.zeros(J.shape, dtype=bool)
                 selfm[:, 0] = True
-            V = self._values(A, J, slots, selfm, r, b, bG, x, st, lo, hi)
-            xn[A] = apply_rule(self.rule, self.t, V, x[A])
+            V, miss = self._values(A, J, slots, selfm, r, b, bG, x, st, lo, hi)
+            xn[A] = self._rule(V, miss, x[A])
         self.x[lb] = xn
         self.hist[lb].append(xn.copy())
         self.rounds[lb] = r + 1
         self._after(lb)
+
+    def _rule(self, V, miss, xi):
+        if self.omit:
+            return apply_rule_omit(self.rule, self.t, V, miss, xi)
+        return apply_rule(self.rule, self.t, V, xi)
 
     def _values(self, A, J, slots, selfm, r, b, bG, x, st, lo, hi):
         """§A.6 resolution of the entry matrix (rows = receivers A, columns = entries)."""
@@ -292,7 +335,7 @@ class NpSim:
                         u = u53(draw(self.seed, BYZS, b, r, s2), draw(self.seed, BYZS, b, r, s2 + np.uint64(1)))
                     V[byzm] = (lo - d) + u * ((hi - lo) + ft(2) * d)
             V[missing | selfm] = np.broadcast_to(x[A][:, None], V.shape)[missing | selfm]
-        return V
+        return V, missing & ~selfm
 
     def round(self, k=1):
         for lb in range(self.B):
