@@ -118,7 +118,7 @@ def gpu_run(cfg, **envs):
     with env(**envs), acsim.Simulator(cfg, device=0) as g:
         name = g.kernel_name()
         g.run()
-        return name, g.rounds(), g.all_values(), g.spread_trace(0)
+        return name, g.rounds(), g.all_values(), g.spread_trace(0) if cfg.trace_spread else None
 
 
 GPU_CASES = [
