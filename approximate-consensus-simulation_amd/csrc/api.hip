@@ -98,6 +98,9 @@ struct acs_sim {
     double2* gpart = nullptr;      // (-min, max) exchanged by all-reduce
     uint64_t* rowptr = nullptr;    // CSR topology (device copies)
     uint32_t* colidx = nullptr;
+    bool csr_var = false;          // CSR on the register / binned paths: padded ELL of a compiled degree
+    uint8_t* deg = nullptr;        // [N] deg(i) (csr_var)
+    uint8_t* sw = nullptr;         // [ceil(N/64)] SELL-64 slice widths in 4-wide groups (csr_var)
     double* dsorted = nullptr;     // dense path: sorted base multiset [N]
     uint32_t* dcounts = nullptr;   // dense path: |B|, #Byzantine, #crash-silent
     std::vector<Part> parts;       // virtual partitions 1..P-1 (partition 0 uses x / ell)
@@ -223,6 +226,8 @@ static void release(acs_sim* s) {
     (void)hipFree(s->gpart);
     (void)hipFree(s->rowptr);
     (void)hipFree(s->colidx);
+    (void)hipFree(s->deg);
+    (void)hipFree(s->sw);
     (void)hipFree(s->dsorted);
     (void)hipFree(s->dcounts);
     (void)hipFree(s->n_done);
@@ -344,6 +349,8 @@ static RoundArgs round_args(acs_sim* s, uint32_t r) {
     a.nblk = s->nblk;
     a.mp = s->mp;
     a.f32 = s->f32 ? 1u : 0u;
+    a.deg = s->deg;
+    a.sw = s->sw;
     return a;
 }
 
@@ -554,6 +561,14 @@ static int advance(acs_sim* s, uint32_t k) {
     return ACS_OK;
 }
 
+// CSR on the register / binned paths (§8(f) row 1): the smallest compiled degree D >= the
+// largest row with the config's (t, rule), 0 if none (the generic kernel then runs).
+static uint32_t csr_fast_degree(uint64_t maxdeg, uint32_t t, uint32_t rule) {
+    for (uint32_t d : {4u, 8u, 16u, 32u})
+        if (d >= maxdeg && regular_fast_supported(d, t, rule)) return d;
+    return 0;
+}
+
 // Build the adjacency rows of partition p into `ell` (sorted when the config allows it).
 static hipError_t build_rows(acs_sim* s, uint32_t* ell, int p) {
     const uint64_t gseed = s->c.graph_seed ? s->c.graph_seed : s->c.seed;
@@ -663,6 +678,13 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     } else if (cfg->topology == ACS_TOPO_RANDOM_REGULAR && regular_fast_supported(s->d, cfg->trim, cfg->rule)) {
         s->path = PATH_REGULAR;
         s->kname = regular_fast_name(s->d, cfg->trim, s->clean);
+    } else if (cfg->topology == ACS_TOPO_CSR && !env_off("ACSIM_CSR_FAST") &&
+               (s->d = csr_fast_degree(csr_mmax - 1, cfg->trim, cfg->rule)) != 0) {
+        // §8(f) row 1: rows padded to the smallest compiled degree >= max deg(i) with the same t
+        s->path = PATH_REGULAR;
+        s->csr_var = true;
+        s->dp = s->d;
+        s->kname = std::string("k_round_regular<") + std::to_string(s->d) + "," + std::to_string(cfg->trim) + ",csr>";
     } else if (s->m <= kGenericMaxM) {
         s->path = PATH_GENERIC;
         s->kname = "k_round_generic";
@@ -691,20 +713,21 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     // multiset), ACSIM_BIN_OF=1: measured slower than the invpos phase B, kept as
     // a tested variant
     const char* of_env = getenv("ACSIM_BIN_OF");
-    const bool bin_of = s->ell_sorted && of_env && of_env[0] == '1';
+    const bool bin_of = s->ell_sorted && of_env && of_env[0] == '1' && !s->csr_var;
     {
         const char* env = getenv("ACSIM_BINNED");
         const bool allow = !(env && env[0] == '0');
         const uint32_t lv = s->path == PATH_REGULAR && s->d ? binned_levels(s->N, rows_local, s->d, bin_sa, nullptr) : 0;
         s->binned = allow && (!s->f32 || s->clean || s->N <= (1ull << 20)) && s->path == PATH_REGULAR && cfg->delay_max == 0 &&
+                    !(s->csr_var && s->f32) &&
                     s->B == 1 && lv != 0 &&
                     binned_supported(s->d, cfg->trim, cfg->rule) && rows_local * s->d < (1ull << 32);
         const char* df = getenv("ACSIM_DEFER_FIN");
         s->defer_fin = s->binned && !partitioned && s->B == 1 && !(df && df[0] == '0');
         if (s->binned) {
             char nm[96];
-            snprintf(nm, sizeof nm, "k_bin_scatter+%sk_bin_gather<%u,%u%s>%s", lv == 2 ? "k_bin_regroup+" : "", s->d,
-                     cfg->trim, s->clean ? "" : ",faulty",
+            snprintf(nm, sizeof nm, "k_bin_scatter+%sk_bin_gather<%u,%u%s%s>%s", lv == 2 ? "k_bin_regroup+" : "", s->d,
+                     cfg->trim, s->clean ? "" : ",faulty", s->csr_var ? ",csr" : "",
                      cfg->fault_model != ACS_FAULT_NONE ? "+k_bin_tag" : "");
             s->kname = nm;
         }
@@ -797,6 +820,21 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         CREATE_TRY(hipMalloc(&s->colidx, (csr_nnz ? csr_nnz : 1) * sizeof(uint32_t)));
         CREATE_TRY(hipMemcpy(s->rowptr, h_rowptr, (s->N + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
         if (csr_nnz) CREATE_TRY(hipMemcpy(s->colidx, h_colidx, csr_nnz * sizeof(uint32_t), hipMemcpyHostToDevice));
+        if (s->csr_var) {   // padded ELL (SELL-64 slice widths), sorted rows when order-free, binned plan
+            const uint64_t words = ((s->N + 63) / 64) * 64ull * s->dp;
+            CREATE_TRY(hipMalloc(&s->ell, words * sizeof(uint32_t)));
+            CREATE_TRY(hipMalloc(&s->deg, s->N));
+            CREATE_TRY(hipMalloc(&s->sw, (s->N + 63) / 64));
+            CREATE_TRY(hipMemsetAsync(s->ell, 0xFF, words * sizeof(uint32_t), s->stream));
+            CREATE_TRY(launch_csr_to_ell(s->rowptr, s->colidx, s->N, s->d, s->ell, s->deg, s->sw, s->stream));
+            if (s->ell_sorted) CREATE_TRY(launch_sort_ell_rows(s->ell, s->N, s->d, s->stream));
+            if (s->binned) {
+                CREATE_TRY(binned_build(s->bin, s->ell, s->N, s->N, s->d, s->dp, bin_sa, tagged, s->f32, false, s->stream,
+                                        true));
+                (void)hipFree(s->ell);
+                s->ell = nullptr;
+            }
+        }
     }
     CREATE_TRY(launch_init_values(s->x[0], s->B, s->N, s->mp.key, cfg->instance_offset, s->f32, s->stream));
     for (Part& q : s->parts)

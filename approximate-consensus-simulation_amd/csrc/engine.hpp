@@ -50,7 +50,14 @@ struct RoundArgs {
     uint64_t xstride;
     uint32_t H, delay;        // delay = D (0: synchronous)
     uint32_t f32;             // ACS_F32: x buffers hold binary32 values
+    // CSR graphs on the register / binned paths (§8(f) row 1): the ELL is padded to the compiled
+    // degree d with kEllNone; deg[i] = deg(i) (< 256), sw[slice] = 4-wide column groups a 64-row
+    // slice actually uses (SELL-64: groups past it are never loaded).  nullptr otherwise.
+    const uint8_t* deg;
+    const uint8_t* sw;
 };
+
+constexpr uint32_t kEllNone = 0xFFFFFFFFu;   // padding column of a CSR row below the compiled degree
 
 struct FinalizeArgs {
     InstState* st;
@@ -90,6 +97,10 @@ hipError_t launch_build_ell(uint32_t* ell, uint64_t N, uint64_t row0, uint64_t n
                             const Feistel& f, hipStream_t s);
 // Sort each ELL row ascending (clean configs with order-independent rules only; d in {4,8,16,32}).
 hipError_t launch_sort_ell_rows(uint32_t* ell, uint64_t N, uint32_t d, hipStream_t s);
+// CSR (§8(f) row 1) -> the padded ELL of width d (a multiple of 4 >= every degree, <= 252), the u8
+// degree of every row and the SELL-64 slice widths (4-wide groups per 64-row slice).
+hipError_t launch_csr_to_ell(const uint64_t* rowptr, const uint32_t* colidx, uint64_t N, uint32_t d, uint32_t* ell,
+                             uint8_t* deg, uint8_t* sw, hipStream_t s);
 hipError_t build_fault_status(uint32_t* status, uint64_t B, uint64_t N, uint32_t f,
                               uint32_t fault_model, uint32_t crash_window, Key key,
                               uint64_t inst_offset, hipStream_t s);
@@ -126,6 +137,7 @@ struct BinnedPlan {
     uint16_t* invpos = nullptr;         // [Q][D/8][kBinSB][8]: position of (receiver, slot) in block b's runs
     uint2* tiles = nullptr;             // [Q][nrun+1] (stage start | pad count, element offset in block b's runs)
     bool ofree = false;                 // order-free phase B (rid, no invpos)
+    bool var = false;                   // CSR rows below the compiled degree (kEllNone columns)
     uint32_t split = 1;                 // phase-B passes over the image (ACSIM_BIN_SPLIT; 1 = whole image)
     uint32_t pol = 0;                   // cache-policy switches (round_binned.hip kPol*)
     uint32_t rstride = 0;               // bytes per receiver block in rid
@@ -144,7 +156,7 @@ uint32_t binned_levels(uint64_t N, uint64_t NR, uint32_t d, uint32_t sa, uint32_
 // need spec order); sa = source block size; tagged: the config has a fault schedule; ofree: clean
 // config under a sort-based rule (order-free phase B: rid instead of invpos).
 hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t NR, uint32_t d, uint32_t dp,
-                        uint32_t sa, bool tagged, bool f32, bool ofree, hipStream_t s);
+                        uint32_t sa, bool tagged, bool f32, bool ofree, hipStream_t s, bool var = false);
 void binned_free(BinnedPlan& p);
 // clean: no slot-dependent decision (selects the plain phase-B instantiation)
 // fin: the previous round's finalize, deferred into this round's phase A (nullptr: none pending)

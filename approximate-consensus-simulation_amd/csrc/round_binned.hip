@@ -247,7 +247,9 @@ __global__ __launch_bounds__(256) void k_bin_tag(const VT* __restrict__ x, const
 template <int D, int NP>
 constexpr uint32_t kBinPartCap = D * kBinSB / NP + D * kBinSB / 16;   // + 1/16 of the image: run-length variation and padding
 
-template <int D, int T, bool WMSR = false, bool FAULTY = false, typename VT = double, int NP = 1>
+// VAR: a CSR graph padded to D (§8(f) row 1): slots t >= deg(i) are absent entries, slot numbers
+// are rowptr[i] + t (one drop draw each); single pass only.
+template <int D, int T, bool WMSR = false, bool FAULTY = false, typename VT = double, int NP = 1, bool VAR = false>
 __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const VT* __restrict__ stage,
                                                        const uint16_t* __restrict__ invpos,
                                                        const uint2* __restrict__ tiles, uint32_t nrun, uint32_t Q,
@@ -275,6 +277,14 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
     uint32_t si = kHonest;
     if constexpr (FAULTY) {
         if (a.status && live) si = a.status[i];
+    }
+    uint32_t dg = D;
+    uint64_t rp = 0;
+    if constexpr (VAR) {
+        if (live) {
+            dg = a.deg[i];
+            if constexpr (FAULTY) rp = a.rowptr[i];
+        }
     }
     uint4 ip[D / 8];
     const uint4* ipp = reinterpret_cast<const uint4*>(invpos) + (uint64_t)b * (D / 8) * kBinSB + threadIdx.x;
@@ -336,6 +346,14 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
         if (!FAULTY || is_active(si, a.r)) {
             v[0] = xi;
             uint32_t nmiss = 0;   // entries left out under missing_policy = OMIT
+            if constexpr (VAR && !FAULTY) {   // absent CSR entries
+#pragma unroll
+                for (int t = 0; t < D; ++t)
+                    if ((uint32_t)t >= dg) {
+                        v[1 + t] = omit_fill<VT>(a.rule);
+                        ++nmiss;
+                    }
+            }
             if constexpr (FAULTY) {   // §A.5 drops, §A.4 / §A.6 sender resolution (round_regular.hip order)
                 const MsgParams& mp = a.mp;
                 const uint32_t bI = (uint32_t)mp.inst_offset, bG = bI - bI % mp.mask_group;
@@ -345,10 +363,18 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
                 for (int q = 0; q < D / 4; ++q) {
                     U4 w;
                     w.v[0] = w.v[1] = w.v[2] = w.v[3] = 0xFFFFFFFFu;
-                    if (mp.thr) w = philox10(iu * (uint32_t)(D / 4) + q, r, bG, kStreamDrop, mp.key);
+                    if (!VAR && mp.thr) w = philox10(iu * (uint32_t)(D / 4) + q, r, bG, kStreamDrop, mp.key);
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const int t = 4 * q + e;
+                        if (VAR && (uint32_t)t >= dg) {   // absent CSR entry
+                            v[1 + t] = omit_fill<VT>(a.rule);
+                            ++nmiss;
+                            continue;
+                        }
+                        const uint64_t slot = VAR ? rp + t : (uint64_t)iu * D + t;
+                        const bool dropped = VAR ? (mp.thr && draw(mp.key, kStreamDrop, bG, r, slot) < mp.thr)
+                                                 : w.v[e] < mp.thr;
                         VT u = v[1 + t];
                         uint32_t stj = kHonest;
                         if constexpr (sizeof(VT) == 8) {
@@ -367,15 +393,14 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
                             }
                         }
                         bool miss;
-                        const VT rv = resolve_entry_m(mp, stj, u, xi, w.v[e] < mp.thr, bI, r, iu, (uint64_t)iu * D + t,
-                                                      lo, hi, miss);
+                        const VT rv = resolve_entry_m(mp, stj, u, xi, dropped, bI, r, iu, slot, lo, hi, miss);
                         const bool out = mp.omit && miss;
                         v[1 + t] = out ? omit_fill<VT>(a.rule) : rv;
                         nmiss += out;
                     }
                 }
             }
-            if (FAULTY && a.mp.omit)
+            if (VAR || (FAULTY && a.mp.omit))
                 res = apply_rule_reg_omit<D, T, WMSR>(a.rule, v, nmiss);
             else
                 res = apply_rule_reg<D, T, WMSR>(a.rule, v);
@@ -555,6 +580,8 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather_of(const RoundArgs a, con
 struct BinGeom {
     uint32_t D, dp, SA, P, Q, levels, SR, R, K, PK, QR;
     uint32_t pad;   // tile lengths padded to 16 bytes: 2 (fp64) or 4 (fp32) elements
+    uint32_t none1, none2;   // tile count of level 1 / 2: the key of an absent CSR column (kEllNone),
+                             // which sorts past every tile and is skipped by every fill kernel
 };
 
 __device__ __forceinline__ uint32_t ell_at(const uint32_t* ell, uint64_t i, uint32_t t, uint32_t dp) {
@@ -567,9 +594,12 @@ __global__ __launch_bounds__(256) void k_bin_keys(const uint32_t* __restrict__ e
     if (e >= E) return;
     const uint64_t li = e / G.D;
     const uint32_t t = (uint32_t)(e % G.D);
-    const uint32_t a = ell_at(ell, li, t, G.dp) / G.SA;
+    const uint32_t col = ell_at(ell, li, t, G.dp);
+    const uint32_t a = col / G.SA;
     uint32_t key;
-    if (G.levels == 1)
+    if (col == kEllNone)
+        key = level == 1 ? G.none1 : G.none2;
+    else if (G.levels == 1)
         key = a * G.Q + (uint32_t)(li / kBinSB);
     else if (level == 1)
         key = a * G.R + (uint32_t)(li / G.SR);
@@ -580,10 +610,12 @@ __global__ __launch_bounds__(256) void k_bin_keys(const uint32_t* __restrict__ e
 }
 
 // tile boundaries in the sorted keys: tl[key] = (first, last+1) unpadded sorted positions
-__global__ __launch_bounds__(256) void k_bin_bounds(uint64_t E, const uint32_t* __restrict__ ks, uint2* __restrict__ tl) {
+__global__ __launch_bounds__(256) void k_bin_bounds(uint64_t E, const uint32_t* __restrict__ ks, uint2* __restrict__ tl,
+                                                    uint64_t nt) {
     const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (p >= E) return;
     const uint32_t key = ks[p];
+    if (key >= nt) return;   // absent CSR columns
     if (p == 0 || ks[p - 1] != key) tl[key].x = (uint32_t)p;
     if (p == E - 1 || ks[p + 1] != key) tl[key].y = (uint32_t)(p + 1);
 }
@@ -605,6 +637,7 @@ __global__ __launch_bounds__(256) void k_bin_fill_a(const uint32_t* __restrict__
     const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (p >= E) return;
     const uint32_t e = vs[p], key = ks[p];
+    if (key >= G.none1) return;
     idxA[pstart[key] + (p - tl[key].x)] = (uint16_t)(ell_at(ell, e / G.D, e % G.D, G.dp) % G.SA);
 }
 
@@ -644,6 +677,7 @@ __global__ __launch_bounds__(256) void k_bin_lpos(uint64_t E, BinGeom G, const u
     const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (p >= E) return;
     const uint32_t key = ks1[p], a = key / G.R, r = key % G.R;
+    if (key >= G.none1) return;
     const uint32_t g = r * G.K + a / G.PK;
     lpos[vs1[p]] = (uint16_t)(mt[(uint64_t)g * (G.PK + 1) + a % G.PK].y + (p - tl1[key].x));
 }
@@ -652,10 +686,11 @@ __global__ __launch_bounds__(256) void k_bin_lpos(uint64_t E, BinGeom G, const u
 __global__ __launch_bounds__(256) void k_bin_fill_m(uint64_t E, const uint32_t* __restrict__ ks2,
                                                     const uint32_t* __restrict__ vs2, const uint2* __restrict__ tl2,
                                                     const uint32_t* __restrict__ pstart2, const uint16_t* __restrict__ lpos,
-                                                    uint16_t* __restrict__ idxM) {
+                                                    uint16_t* __restrict__ idxM, uint32_t none2) {
     const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (p >= E) return;
     const uint32_t key = ks2[p];
+    if (key >= none2) return;
     idxM[pstart2[key] + (p - tl2[key].x)] = lpos[vs2[p]];
 }
 
@@ -700,6 +735,7 @@ __global__ __launch_bounds__(256) void k_bin_inv(uint64_t E, BinGeom G, uint32_t
     const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (p >= E) return;
     const uint32_t e = vs[p], key = ks[p];
+    if (key >= (G.levels == 1 ? G.none1 : G.none2)) return;
     const uint64_t li = e / G.D;
     const uint32_t t = e % G.D;
     const uint32_t b = (uint32_t)(li / kBinSB);
@@ -716,6 +752,7 @@ __global__ __launch_bounds__(256) void k_bin_rid(uint64_t E, BinGeom G, uint32_t
     const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (p >= E) return;
     const uint32_t e = vs[p], key = ks[p];
+    if (key >= (G.levels == 1 ? G.none1 : G.none2)) return;
     const uint64_t li = e / G.D;
     const uint32_t b = (uint32_t)(li / kBinSB);
     const uint32_t j = G.levels == 1 ? key / G.Q : (key / G.QR) % G.K;
@@ -795,7 +832,7 @@ hipError_t tile_sort(const uint32_t* ell, uint64_t E, const BinGeom& G, int leve
     void* temp = nullptr;
     size_t tb = 0, tb2 = 0;
     int bits = 1;
-    while (bits < 32 && (1ull << bits) < nt) ++bits;
+    while (bits < 32 && (1ull << bits) <= nt) ++bits;   // keys 0..nt (nt: absent CSR columns)
     const unsigned grid = (unsigned)((E + 255) / 256), gridt = (unsigned)((nt + 255) / 256);
     e = hipMalloc(&keys, E * 4);
     if (e == hipSuccess) e = hipMalloc(&vals, E * 4);
@@ -815,7 +852,7 @@ hipError_t tile_sort(const uint32_t* ell, uint64_t E, const BinGeom& G, int leve
     if (e == hipSuccess) e = hipMalloc(&temp, tb ? tb : 16);
     if (e == hipSuccess) e = hipcub::DeviceRadixSort::SortPairs(temp, tb, keys, T.ks, vals, T.vs, (int)E, 0, bits, s);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_bin_bounds, dim3(grid), dim3(256), 0, s, E, T.ks, T.tl);
+        hipLaunchKernelGGL(k_bin_bounds, dim3(grid), dim3(256), 0, s, E, T.ks, T.tl, nt);
         hipLaunchKernelGGL(k_bin_plen, dim3(gridt), dim3(256), 0, s, T.tl, nt, G.pad, T.plen);
         e = hipGetLastError();
     }
@@ -835,7 +872,8 @@ hipError_t tile_sort(const uint32_t* ell, uint64_t E, const BinGeom& G, int leve
 }  // namespace
 
 hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t NR, uint32_t d, uint32_t dp,
-                        uint32_t sa, bool tagged, bool f32, bool ofree, hipStream_t s) {
+                        uint32_t sa, bool tagged, bool f32, bool ofree, hipStream_t s, bool var) {
+    if (var && (f32 || ofree)) return hipErrorNotSupported;   // CSR plans: fp64, invpos phase B
     hipError_t e = hipSuccess;
     uint32_t sr = 0;
     const uint32_t levels = binned_levels(N, NR, d, sa, &sr);
@@ -860,6 +898,9 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
         G.PK = pk < 1 ? 1 : pk > G.P ? G.P : pk;
     }
     G.K = (G.P + G.PK - 1) / G.PK;
+    G.none1 = G.P * G.R;
+    G.none2 = levels == 2 ? G.R * G.K * G.QR : 0;
+    p.var = var;
     p.D = d;
     p.SA = sa;
     p.f32 = f32;
@@ -921,7 +962,8 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
         if (e == hipSuccess) e = hipMalloc(&p.stage2, p.Ep2 * (f32 ? sizeof(float) : sizeof(double)));
         if (e == hipSuccess) e = hipMalloc(&p.moff, ((uint64_t)ng + 1) * sizeof(uint64_t));
         if (e == hipSuccess) {
-            hipLaunchKernelGGL(k_bin_fill_m, dim3(grid), dim3(256), 0, s, E, T2.ks, T2.vs, T2.tl, T2.pstart, lpos, p.idxM);
+            hipLaunchKernelGGL(k_bin_fill_m, dim3(grid), dim3(256), 0, s, E, T2.ks, T2.vs, T2.tl, T2.pstart, lpos, p.idxM,
+                               G.none2);
             hipLaunchKernelGGL(k_bin_moff, dim3((ng + 256) / 256), dim3(256), 0, s, T2.pstart, G, p.Ep2, p.moff);
             e = hipGetLastError();
         }
@@ -972,7 +1014,7 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     if (e == hipSuccess && !ofree) {
         const char* v = getenv("ACSIM_BIN_SPLIT");
         uint32_t np = v ? (uint32_t)strtoul(v, nullptr, 10) : (!f32 && G.D == 32 ? 2u : 1u);
-        if (np < 1 || np > 4) np = 1;
+        if (np < 1 || np > 4 || var) np = 1;   // CSR plans: single pass (the VAR kernels)
         if (f32 && tagged && np > 1) np = 1;   // tagged fp32 phase B: one pass (no split instantiation)
         if (tagged && np > 2) np = 2;          // tagged fp64 phase B: two passes at most
         if (np > 1) {
@@ -1144,7 +1186,19 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
 #define X(DD, TT)                                                                                        \
     if (p.D == DD && a.trim == TT) {                                                                     \
         const bool w_ = a.rule == 4;                                                                     \
-        if (clean && p.ofree && w_)                                                                      \
+        if (p.var && clean && w_)                                                                        \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, true, false, double, 1, true>), grid, dim3(kBinSB), 0, s, \
+                               a, last, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                             \
+        else if (p.var && clean)                                                                         \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, false, false, double, 1, true>), grid, dim3(kBinSB), 0, s, \
+                               a, last, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                             \
+        else if (p.var && w_)                                                                            \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, true, true, double, 1, true>), grid, dim3(kBinSB), 0, s, \
+                               a, last, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                             \
+        else if (p.var)                                                                                  \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, false, true, double, 1, true>), grid, dim3(kBinSB), 0, s, \
+                               a, last, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                             \
+        else if (clean && p.ofree && w_)                                                                      \
             hipLaunchKernelGGL((k_bin_gather_of<DD, TT, true>), grid, dim3(kBinSB), 0, s, a, last, p.rid,   \
                                p.rstride, p.tiles, p.nrun, p.Q, Qc);                                     \
         else if (clean && p.ofree)                                                                       \

@@ -18,7 +18,10 @@
 namespace acs {
 
 // VT = double, or float in fp32 mode (4-byte gathers, binary32 rule arithmetic).
-template <int D, int T, bool CLEAN, bool WMSR = false, typename VT = double>
+// VAR: a CSR graph (§8(f) row 1) padded to D (SELL-64: column groups past the slice's widest row
+// are not loaded; columns past deg(i) are absent entries; slot s = rowptr[i] + t, one draw per
+// slot).  VAR kernels always take the resolving (non-CLEAN) body.
+template <int D, int T, bool CLEAN, bool WMSR = false, typename VT = double, bool VAR = false>
 __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs a) {
     static_assert(D % 4 == 0, "compiled degrees are multiples of 4");
     constexpr int M = D + 1;
@@ -51,9 +54,16 @@ __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs
             const uint4* cp = reinterpret_cast<const uint4*>(a.ell) +
                               (uint64_t)(li >> 6) * (NQ * 64) + (li & 63);
             uint32_t col[D];
+            uint32_t nqs = NQ, dg = D;
+            uint64_t rp = 0;
+            if constexpr (VAR) {
+                nqs = a.sw[li >> 6];   // uniform over the wave (one 64-row slice)
+                dg = a.deg[i];
+                rp = a.rowptr[i];
+            }
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
-                const uint4 c = cp[q * 64];
+                const uint4 c = (!VAR || (uint32_t)q < nqs) ? cp[q * 64] : make_uint4(kEllNone, kEllNone, kEllNone, kEllNone);
                 col[4 * q + 0] = c.x;
                 col[4 * q + 1] = c.y;
                 col[4 * q + 2] = c.z;
@@ -74,7 +84,18 @@ __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs
                 VT xj[D];
                 uint32_t sj[D];
                 // all gathers first, unconditionally (the branch is uniform and hoisted)
-                if (a.delay) {   // bounded delay: one DELAY Philox call per 4 slots, history gathers
+                if constexpr (VAR) {   // CSR: absent columns load nothing (their entries are filled below)
+#pragma unroll
+                    for (int t = 0; t < D; ++t) {
+                        const bool ok = (uint32_t)t < dg;
+                        const uint32_t j = ok ? col[t] : i;
+                        if (a.delay)
+                            xj[t] = ok ? delayed_x<VT>(a, lb, r, draw(mp.key, kStreamDelay, b, r, rp + t), j) : xi;
+                        else
+                            xj[t] = ok ? x[j] : xi;
+                        sj[t] = (ok && stv) ? stv[j] : kHonest;
+                    }
+                } else if (a.delay) {   // bounded delay: one DELAY Philox call per 4 slots, history gathers
 #pragma unroll
                     for (int q = 0; q < NQ; ++q) {
                         const U4 wd = philox10(i * (uint32_t)NQ + q, r, b, kStreamDelay, mp.key);
@@ -100,15 +121,22 @@ __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs
                 }
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
-                    // slots s = i*D + 4q .. +3 share Philox counter s>>2 = i*(D/4) + q (§A.5)
+                    // slots s = i*D + 4q .. +3 share Philox counter s>>2 = i*(D/4) + q (§A.5); CSR
+                    // slots rowptr[i] + t are not 4-aligned: one draw each
                     U4 w;
                     w.v[0] = w.v[1] = w.v[2] = w.v[3] = 0xFFFFFFFFu;
-                    if (mp.thr) w = philox10(i * (uint32_t)NQ + q, r, bG, kStreamDrop, mp.key);
+                    if (!VAR && mp.thr) w = philox10(i * (uint32_t)NQ + q, r, bG, kStreamDrop, mp.key);
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const int t = 4 * q + e;
-                        const uint64_t s = (uint64_t)i * D + t;
-                        const bool dropped = w.v[e] < mp.thr;
+                        const uint64_t s = VAR ? rp + t : (uint64_t)i * D + t;
+                        if (VAR && (uint32_t)t >= dg) {   // absent entry (not in S_i at all)
+                            v[1 + t] = omit_fill<VT>(a.rule);
+                            ++nmiss;
+                            continue;
+                        }
+                        const bool dropped = VAR ? (mp.thr && draw(mp.key, kStreamDrop, bG, r, s) < mp.thr)
+                                                 : w.v[e] < mp.thr;
                         bool miss;
                         const VT u = resolve_entry_m(mp, sj[t], xj[t], xi, dropped, b, r, i, s, lo, hi, miss);
                         const bool out = mp.omit && miss;
@@ -117,7 +145,7 @@ __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs
                     }
                 }
             }
-            if (!CLEAN && a.mp.omit)
+            if (!CLEAN && (VAR || a.mp.omit))
                 res = apply_rule_reg_omit<D, T, WMSR>(a.rule, v, nmiss);
             else
                 res = apply_rule_reg<D, T, WMSR>(a.rule, v);
@@ -134,7 +162,11 @@ __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs
 template <int D, int T, typename VT>
 static void launch_regular_t(const RoundArgs& a, dim3 grid, dim3 block, bool clean, hipStream_t s) {
     const bool w = a.rule == 4;
-    if (clean && w)
+    if (a.deg && w)
+        hipLaunchKernelGGL((k_round_regular<D, T, false, true, VT, true>), grid, block, 0, s, a);
+    else if (a.deg)
+        hipLaunchKernelGGL((k_round_regular<D, T, false, false, VT, true>), grid, block, 0, s, a);
+    else if (clean && w)
         hipLaunchKernelGGL((k_round_regular<D, T, true, true, VT>), grid, block, 0, s, a);
     else if (clean)
         hipLaunchKernelGGL((k_round_regular<D, T, true, false, VT>), grid, block, 0, s, a);

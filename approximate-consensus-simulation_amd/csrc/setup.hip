@@ -76,6 +76,36 @@ hipError_t launch_sort_ell_rows(uint32_t* ell, uint64_t N, uint32_t d, hipStream
     return hipGetLastError();
 }
 
+// §8(f) row 1: CSR rows as the padded ELL slice layout of the register / binned paths.
+__global__ __launch_bounds__(256) void k_csr_to_ell(const uint64_t* __restrict__ rowptr, const uint32_t* __restrict__ colidx,
+                                                    uint64_t N, uint32_t d, uint32_t* __restrict__ ell,
+                                                    uint8_t* __restrict__ deg) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= N) return;
+    const uint64_t rp = rowptr[i];
+    const uint32_t dg = (uint32_t)(rowptr[i + 1] - rp);
+    deg[i] = (uint8_t)dg;
+    for (uint32_t t = 0; t < d; ++t)
+        ell[(((i >> 6) * (d >> 2) + (t >> 2)) * 64 + (i & 63)) * 4 + (t & 3)] = t < dg ? colidx[rp + t] : kEllNone;
+}
+
+// SELL-64 slice widths: 4-wide column groups used by the longest row of each 64-row slice
+__global__ __launch_bounds__(256) void k_slice_width(const uint8_t* __restrict__ deg, uint64_t N, uint8_t* __restrict__ sw) {
+    const uint64_t sl = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (sl * 64 >= N) return;
+    uint32_t mx = 0;
+    for (uint64_t k = sl * 64; k < N && k < sl * 64 + 64; ++k) mx = deg[k] > mx ? deg[k] : mx;
+    sw[sl] = (uint8_t)((mx + 3) / 4);
+}
+
+hipError_t launch_csr_to_ell(const uint64_t* rowptr, const uint32_t* colidx, uint64_t N, uint32_t d, uint32_t* ell,
+                             uint8_t* deg, uint8_t* sw, hipStream_t s) {
+    hipLaunchKernelGGL(k_csr_to_ell, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, rowptr, colidx, N, d, ell, deg);
+    const uint64_t ns = (N + 63) / 64;
+    hipLaunchKernelGGL(k_slice_width, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, s, deg, N, sw);
+    return hipGetLastError();
+}
+
 __global__ __launch_bounds__(256) void k_fault_keys(uint64_t* keys, uint64_t N, Key key, uint64_t inst_offset) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const uint32_t lb = blockIdx.y;

@@ -95,3 +95,108 @@ def test_csr_gpu_matches_oracle(oracle_mod, kw):
         assert np.array_equal(g.values(0).view(np.uint64), o.values(0).view(np.uint64))
         assert np.array_equal(g.spread_trace(0).view(np.uint64), o.spread_trace(0).view(np.uint64))
         assert np.array_equal(g.fault_status(), o.fault_status())
+
+
+# --------------------------------------------------------------------------- CSR fast path
+# Rows padded to the smallest compiled degree D >= max deg(i) (SELL-64 slices on the per-lane
+# register kernel; variable-degree phase B on the binned exchange): bit-exact vs the oracle.
+import contextlib  # noqa: E402
+import os  # noqa: E402
+
+
+@contextlib.contextmanager
+def env(**kw):
+    old = {k: os.environ.get(k) for k in kw}
+    os.environ.update({k: str(v) for k, v in kw.items()})
+    try:
+        yield
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def skewed_csr(N, dmin, dmax, seed, alpha=2.0):
+    """Power-law degrees in [dmin, dmax] (most rows near dmin, a tail up to dmax) and senders drawn
+    half uniformly, half from a small hub set: skewed in-degree too."""
+    rng = np.random.default_rng(seed)
+    u = rng.random(N)
+    deg = np.floor(dmin * (1 - u * (1 - (dmin / (dmax + 1)) ** (alpha - 1))) ** (-1 / (alpha - 1))).astype(np.int64)
+    deg = np.clip(deg, dmin, dmax)
+    rowptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.uint64)
+    nnz = int(rowptr[-1])
+    hubs = rng.integers(0, N, size=max(1, N // 100))
+    col = np.where(rng.random(nnz) < 0.5, rng.integers(0, N, size=nnz), hubs[rng.integers(0, hubs.size, size=nnz)])
+    return rowptr, col.astype(np.uint32)
+
+
+FAST = [
+    ("trim5_clean", dict(rule="trimmed", trim=5), (11, 32)),
+    ("mid2_byz_drop", dict(rule="midpoint", trim=2, fault_model="byzantine", n_faulty=60, byz_strategy="random",
+                           byz_delta=0.1, loss_p=0.2), (5, 8)),
+    ("avg_crash_drop", dict(rule="average", fault_model="crash", n_faulty=80, crash_window=5, loss_p=0.15), (3, 16)),
+    ("dlpsw5_split", dict(rule="dlpsw", trim=5, fault_model="byzantine", n_faulty=40, byz_strategy="split",
+                          byz_delta=0.2), (12, 32)),
+    ("wmsr5_clean", dict(rule="wmsr", trim=5), (11, 16)),
+    ("trim2_omit_loss", dict(rule="trimmed", trim=2, loss_p=0.4, missing_policy="omit"), (5, 8)),
+    ("avg_clean", dict(rule="average"), (2, 32)),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["per_lane", "binned"])
+@pytest.mark.parametrize("name,kw,degs", FAST, ids=[f[0] for f in FAST])
+def test_csr_fast_path_matches_oracle(oracle_mod, name, kw, degs, path):
+    N = 20000
+    rowptr, colidx = skewed_csr(N, degs[0], degs[1], 7)
+    cfg = Config(n_nodes=N, topology="csr", eps=1e-9, seed=8, trace_spread=True, **{"max_rounds": 300, **kw})
+    envs = {"ACSIM_BINNED": 0} if path == "per_lane" else {"ACSIM_BIN_SA": 1024}
+    with env(**envs), acsim.Simulator(cfg, csr=(rowptr, colidx)) as g:
+        kname = g.kernel_name()
+        g.run()
+        gr, gx, gt = g.rounds(), g.values(0), g.spread_trace(0)
+    assert ("k_round_regular" if path == "per_lane" else "k_bin_scatter") in kname and "csr" in kname, kname
+    with oracle_mod.OracleSimulator(cfg, threads=8, csr=(rowptr, colidx)) as o:
+        o.run()
+        assert np.array_equal(gr, o.rounds())
+        assert np.array_equal(gx.view(np.uint64), o.values(0).view(np.uint64))
+        assert np.array_equal(gt.view(np.uint64), o.spread_trace(0).view(np.uint64))
+
+
+@pytest.mark.gpu
+def test_csr_fast_path_multi_instance_delay_f32(oracle_mod):
+    """The per-lane CSR kernel with 3 instances and bounded delays, and in fp32."""
+    rowptr, colidx = skewed_csr(5000, 5, 16, 9)
+    for kw in (dict(n_instances=3, rule="trimmed", trim=5, loss_p=0.1, delay_max=2),
+               dict(rule="trimmed", trim=5, fault_model="crash", n_faulty=100, crash_window=3, loss_p=0.1,
+                    dtype="f32")):
+        cfg = Config(n_nodes=5000, topology="csr", eps=1e-7, seed=10, max_rounds=300, **kw)
+        with acsim.Simulator(cfg, csr=(rowptr, colidx)) as g, \
+                oracle_mod.OracleSimulator(cfg, threads=8, csr=(rowptr, colidx)) as o:
+            assert "csr" in g.kernel_name(), g.kernel_name()
+            g.run()
+            o.run()
+            assert np.array_equal(g.rounds(), o.rounds())
+            bt = np.uint64 if cfg.dtype == "f64" else np.uint32
+            assert np.array_equal(g.all_values().view(bt), o.all_values().view(bt))
+
+
+@pytest.mark.gpu
+def test_csr_full_size_skewed_2e20(oracle_mod):
+    """2^20 nodes, power-law degrees 11..32 and hub-skewed senders, trimmed t = 5 (the headline
+    rule on a user graph): the binned CSR path, 12 FIXED rounds, bit-exact vs the oracle."""
+    N = 1 << 20
+    rowptr, colidx = skewed_csr(N, 11, 32, 11)
+    cfg = Config(n_nodes=N, topology="csr", rule="trimmed", trim=5, termination="fixed", max_rounds=12, seed=12,
+                 trace_spread=True)
+    with acsim.Simulator(cfg, csr=(rowptr, colidx)) as g:
+        kname = g.kernel_name()
+        g.run()
+        gx, gt = g.values(0), g.spread_trace(0)
+    assert kname.startswith("k_bin_scatter") and "csr" in kname, kname
+    with oracle_mod.OracleSimulator(cfg, threads=16, csr=(rowptr, colidx)) as o:
+        o.run()
+        assert np.array_equal(gx.view(np.uint64), o.values(0).view(np.uint64))
+        assert np.array_equal(gt.view(np.uint64), o.spread_trace(0).view(np.uint64))
