@@ -15,12 +15,7 @@ from acsim import _abi
 from acsim.config import Config
 
 
-def random_csr(N, dmin, dmax, seed):
-    rng = np.random.default_rng(seed)
-    deg = rng.integers(dmin, dmax + 1, size=N)
-    rowptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.uint64)
-    colidx = rng.integers(0, N, size=int(rowptr[-1])).astype(np.uint32)
-    return rowptr, colidx
+from acsim.graphs import random_csr, skewed_csr  # noqa: E402
 
 
 CASES = [
@@ -118,20 +113,6 @@ def env(**kw):
                 os.environ[k] = v
 
 
-def skewed_csr(N, dmin, dmax, seed, alpha=2.0):
-    """Power-law degrees in [dmin, dmax] (most rows near dmin, a tail up to dmax) and senders drawn
-    half uniformly, half from a small hub set: skewed in-degree too."""
-    rng = np.random.default_rng(seed)
-    u = rng.random(N)
-    deg = np.floor(dmin * (1 - u * (1 - (dmin / (dmax + 1)) ** (alpha - 1))) ** (-1 / (alpha - 1))).astype(np.int64)
-    deg = np.clip(deg, dmin, dmax)
-    rowptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.uint64)
-    nnz = int(rowptr[-1])
-    hubs = rng.integers(0, N, size=max(1, N // 100))
-    col = np.where(rng.random(nnz) < 0.5, rng.integers(0, N, size=nnz), hubs[rng.integers(0, hubs.size, size=nnz)])
-    return rowptr, col.astype(np.uint32)
-
-
 FAST = [
     ("trim5_clean", dict(rule="trimmed", trim=5), (11, 32)),
     ("mid2_byz_drop", dict(rule="midpoint", trim=2, fault_model="byzantine", n_faulty=60, byz_strategy="random",
@@ -168,7 +149,7 @@ def test_csr_fast_path_matches_oracle(oracle_mod, name, kw, degs, path):
 @pytest.mark.gpu
 def test_csr_fast_path_multi_instance_delay_f32(oracle_mod):
     """The per-lane CSR kernel with 3 instances and bounded delays, and in fp32."""
-    rowptr, colidx = skewed_csr(5000, 5, 16, 9)
+    rowptr, colidx = skewed_csr(5000, 11, 16, 9)
     for kw in (dict(n_instances=3, rule="trimmed", trim=5, loss_p=0.1, delay_max=2),
                dict(rule="trimmed", trim=5, fault_model="crash", n_faulty=100, crash_window=3, loss_p=0.1,
                     dtype="f32")):

@@ -27,16 +27,28 @@ CASES = {
     "cfg3_f32": dict(),
     "cfg5_f32": dict(max_rounds=20),   # fp32 two-level plan
     "cfg4_byz_f32": dict(),            # fp32 tagged binned exchange
+    "cfg4_fixed14": dict(max_rounds=14),   # the FIXED twin of cfg4_eps's 14 rounds (EPS overhead check)
+    # user graph (§8(f) row 1): 2^20 nodes, power-law degrees 11..32, hub-skewed senders, trimmed t=5
+    "csr_2e20": dict(max_rounds=20),
+    "csr_2e20_generic": dict(max_rounds=20),   # the same graph on the one-workgroup-per-receiver kernel
 }
 
 
 def run(name, **kw):
-    if name.endswith("_f32"):
+    csr = None
+    if name.startswith("csr_2e20"):
+        from acsim.graphs import skewed_csr
+        csr = skewed_csr(1 << 20, 11, 32, 11)
+        cfg = acsim.Config(n_nodes=1 << 20, topology="csr", rule="trimmed", trim=5, termination="fixed", **kw)
+        os.environ["ACSIM_CSR_FAST"] = "0" if name.endswith("_generic") else "1"
+    elif name == "cfg4_fixed14":
+        cfg = acsim.preset("cfg4", **kw)
+    elif name.endswith("_f32"):
         cfg = acsim.preset(name[:-4], dtype="f32", **kw)
     else:
         cfg = acsim.preset(name, **kw)
     t0 = time.perf_counter()
-    sim = acsim.Simulator(cfg)
+    sim = acsim.Simulator(cfg, csr=csr)
     t_setup = time.perf_counter() - t0
     sim.set_kernel_timing(True, every=10)
     t0 = time.perf_counter()
