@@ -96,6 +96,15 @@ struct acs_sim {
     uint64_t rows_per = 0, Npad = 0;
     ncclComm_t comm = nullptr;
     double2* gpart = nullptr;      // (-min, max) exchanged by all-reduce
+    // chunked exchange (binned partitions): the round's rows in xchunks row chunks;
+    // chunk k is sent on cstream as soon as its phase B finishes, and the next round's phase A for
+    // the source blocks of chunk k starts as soon as chunk k has arrived from every rank
+    uint32_t xchunks = 0;          // 0: the unchunked sequence (all-gather after the round)
+    uint32_t bin_sa = 0;           // source-block size of the binned plans (chunks align to it)
+    hipStream_t cstream = nullptr;
+    static constexpr uint32_t kMaxX = 8;
+    hipEvent_t ev_b[kMaxX] = {}, ev_x[kMaxX] = {};
+    hipEvent_t ev_fin = nullptr;
     uint64_t* rowptr = nullptr;    // CSR topology (device copies)
     uint32_t* colidx = nullptr;
     bool csr_var = false;          // CSR on the register / binned paths: padded ELL of a compiled degree
@@ -209,7 +218,14 @@ static void release(acs_sim* s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
+    if (s->cstream) (void)hipStreamSynchronize(s->cstream);
     if (s->comm) (void)ncclCommDestroy(s->comm);
+    for (uint32_t k = 0; k < acs_sim::kMaxX; ++k) {
+        if (s->ev_b[k]) (void)hipEventDestroy(s->ev_b[k]);
+        if (s->ev_x[k]) (void)hipEventDestroy(s->ev_x[k]);
+    }
+    if (s->ev_fin) (void)hipEventDestroy(s->ev_fin);
+    if (s->cstream) (void)hipStreamDestroy(s->cstream);
     for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
     for (Part& p : s->parts) {
         (void)hipFree(p.x[0]);
@@ -351,11 +367,122 @@ static RoundArgs round_args(acs_sim* s, uint32_t r) {
     a.f32 = s->f32 ? 1u : 0u;
     a.deg = s->deg;
     a.sw = s->sw;
+    a.qlo = 0;
+    a.qhi = 0xFFFFFFFFu;
     return a;
+}
+
+static uint64_t chunk_rows(const acs_sim* s, int p, uint32_t k) {
+    const uint64_t cs = s->rows_per / s->xchunks, n = part_rows(s, p), lo = (uint64_t)k * cs;
+    return n > lo ? (n - lo < cs ? n - lo : cs) : 0;
+}
+
+// Chunked node-partitioned round on the binned path.  Compute stream: phase A by
+// source-block chunk (chunk k of every rank, after round r-1's exchange of chunk k), phase M, then
+// phase B by receiver-block chunk (after round r-1's verdict, so a finished run's phase B exits).
+// Comm stream: each chunk's exchange as soon as its phase B is done (RCCL grouped send / recv to
+// every peer over xGMI, or device copies between virtual partitions), then the spread fold,
+// all-reduce and verdict.  Phase A / M of round r+1 may run before round r's verdict: they only
+// write the stage, and phase B (the only writer of x) waits for the verdict.
+static int enqueue_round_xchunked(acs_sim* s, uint32_t r) {
+    const RoundArgs a = round_args(s, r);
+    const uint32_t K = s->xchunks;
+    const uint64_t cs = s->rows_per / K;
+    const uint32_t SA = s->bin_sa;
+    const uint32_t bpr = (uint32_t)(s->rows_per / SA), bpc = (uint32_t)(cs / SA);
+    const uint32_t qpc = (uint32_t)(cs / kBinSB);
+    const int nparts = s->virt ? s->nranks : 1;
+    auto pargs = [&](int p) {
+        RoundArgs ap = a;
+        const int g = s->virt ? p : s->rank;
+        if (s->virt && p > 0) {
+            ap.xin = s->parts[p - 1].x[r & 1u];
+            ap.xout = s->parts[p - 1].x[(r + 1) & 1u];
+        }
+        ap.row0 = part_row0(s, g);
+        ap.nrows = part_rows(s, g);
+        if (s->virt) ap.partial = s->partial + (uint64_t)p * s->nblk;
+        return ap;
+    };
+    auto plan = [&](int p) -> const BinnedPlan& { return (s->virt && p > 0) ? s->parts[p - 1].bin : s->bin; };
+    hipEvent_t e1;
+    int rc = timing_begin(s, &e1);
+    if (rc) return rc;
+    for (uint32_t k = 0; k < K; ++k) {
+        HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_x[k], 0));
+        for (int p = 0; p < nparts; ++p)
+            if (pargs(p).nrows)
+                HIP_TRY(launch_round_binned(plan(p), pargs(p), s->clean, s->stream, nullptr, 1u,
+                                            SrcSel{(uint32_t)s->nranks * bpc, bpr, bpc, k * bpc}));
+    }
+    for (int p = 0; p < nparts; ++p)
+        if (pargs(p).nrows) HIP_TRY(launch_round_binned(plan(p), pargs(p), s->clean, s->stream, nullptr, 2u));
+    HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_fin, 0));
+    const ncclDataType_t dt = s->f32 ? ncclFloat32 : ncclFloat64;
+    for (uint32_t k = 0; k < K; ++k) {
+        for (int p = 0; p < nparts; ++p) {
+            RoundArgs ap = pargs(p);
+            if (!ap.nrows) continue;
+            ap.qlo = k * qpc;
+            ap.qhi = k + 1 == K ? 0xFFFFFFFFu : (k + 1) * qpc;
+            HIP_TRY(launch_round_binned(plan(p), ap, s->clean, s->stream, nullptr, 4u));
+        }
+        HIP_TRY(hipEventRecord(s->ev_b[k], s->stream));
+        HIP_TRY(hipStreamWaitEvent(s->cstream, s->ev_b[k], 0));
+        if (s->virt) {   // chunk k of every partition into every other partition's copy
+            const uint32_t o = (r + 1) & 1u;
+            for (int p = 0; p < s->nranks; ++p) {
+                const uint64_t n = chunk_rows(s, p, k), off = part_row0(s, p) + (uint64_t)k * cs;
+                if (!n) continue;
+                const double* src = p == 0 ? s->x[o] : s->parts[p - 1].x[o];
+                for (int q = 0; q < s->nranks; ++q) {
+                    if (q == p) continue;
+                    double* dst = q == 0 ? s->x[o] : s->parts[q - 1].x[o];
+                    HIP_TRY(hipMemcpyAsync(xat(s, dst, off), xat(s, src, off), n * s->es, hipMemcpyDeviceToDevice,
+                                           s->cstream));
+                }
+            }
+        } else if (s->nranks > 1) {
+            double* xo = s->x[(r + 1) & 1u];
+            NCCL_TRY(ncclGroupStart());
+            for (int q = 0; q < s->nranks; ++q) {
+                if (q == s->rank) continue;
+                const uint64_t mine = chunk_rows(s, s->rank, k), theirs = chunk_rows(s, q, k);
+                if (mine)
+                    NCCL_TRY(ncclSend(xat(s, xo, part_row0(s, s->rank) + (uint64_t)k * cs), mine, dt, q, s->comm,
+                                      s->cstream));
+                if (theirs)
+                    NCCL_TRY(ncclRecv(xat(s, xo, part_row0(s, q) + (uint64_t)k * cs), theirs, dt, q, s->comm,
+                                      s->cstream));
+            }
+            NCCL_TRY(ncclGroupEnd());
+        }
+        HIP_TRY(hipEventRecord(s->ev_x[k], s->cstream));
+    }
+    if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
+    // verdict of round r on the comm stream (it has waited for every phase-B chunk)
+    if (s->virt) {
+        uint32_t nblk_live = 0;
+        for (int p = 0; p < s->nranks; ++p)
+            if (part_rows(s, p)) nblk_live = (uint32_t)((p + 1) * s->nblk);
+        HIP_TRY(launch_finalize(make_finalize(s, r + 1, s->partial, nblk_live, false), s->B, s->cstream));
+    } else {
+        FinalizeArgs fold = make_finalize(s, r + 1, s->partial, a.nrows ? s->nblk : 0, false);
+        fold.fold_out = s->gpart;
+        if (!part_rows(s, s->rank)) fold.nblk = 0;
+        HIP_TRY(launch_finalize(fold, s->B, s->cstream));
+        if (s->nranks > 1) NCCL_TRY(ncclAllReduce(s->gpart, s->gpart, 2, ncclFloat64, ncclMax, s->comm, s->cstream));
+        FinalizeArgs fin = make_finalize(s, r + 1, s->gpart, 1, false);
+        fin.negmin = 1;
+        HIP_TRY(launch_finalize(fin, s->B, s->cstream));
+    }
+    HIP_TRY(hipEventRecord(s->ev_fin, s->cstream));
+    return ACS_OK;
 }
 
 // One round x^r -> x^{r+1}: round kernel(s), [exchange], spread finalize.
 static int enqueue_round(acs_sim* s, uint32_t r) {
+    if (s->xchunks) return enqueue_round_xchunked(s, r);
     RoundArgs a = round_args(s, r);
     hipEvent_t e1;
     int rc = timing_begin(s, &e1);
@@ -526,6 +653,10 @@ static int advance(acs_sim* s, uint32_t k) {
         return ACS_OK;
     }
     const bool eps_mode = s->c.termination == ACS_TERM_EPS;
+    // Long rounds (a chunk of them takes milliseconds): wait for each chunk's verdict before
+    // enqueuing the next, so no chunk of no-op launches follows convergence (the host wake-up is
+    // < 1 % of a chunk).  Short rounds keep one chunk in flight and poll the previous one.
+    const bool sync_poll = eps_mode && s->N * (uint64_t)(s->d ? s->d : s->m) * s->B >= (1ull << 22);
     int slot = 0, prev = -1;
     hipEvent_t poll[2] = {nullptr, nullptr};
     while (k > 0 && !s->all_done) {
@@ -536,10 +667,15 @@ static int advance(acs_sim* s, uint32_t k) {
             if (rc) return rc;
         }
         if (int rc = flush_finalize(s)) return rc;
+        if (s->xchunks) HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_fin, 0));   // verdicts land on cstream
         s->round += chunk;
         k -= chunk;
         if (s->round >= s->c.max_rounds) break;
-        if (eps_mode) {
+        if (sync_poll && k > 0) {
+            HIP_TRY(hipMemcpyAsync(s->h_ndone, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+            HIP_TRY(hipStreamSynchronize(s->stream));
+            if (s->h_ndone[0] == s->B) s->all_done = true;
+        } else if (eps_mode && !sync_poll) {
             // keep one chunk in flight: poll the previous chunk's done counter
             HIP_TRY(hipMemcpyAsync(s->h_ndone + slot, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost,
                                    s->stream));
@@ -840,6 +976,28 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     for (Part& q : s->parts)
         CREATE_TRY(launch_init_values(q.x[0], s->B, s->N, s->mp.key, cfg->instance_offset, s->f32, s->stream));
 #undef CREATE_TRY
+    // chunked exchange: clean binned partitions whose row blocks split into
+    // ACSIM_XCHUNKS (default 4) chunks of whole source blocks; 0 or 1 keeps the unchunked sequence
+    if (partitioned && s->binned && s->clean) {
+        uint32_t K = 4;
+        if (const char* v = getenv("ACSIM_XCHUNKS")) K = (uint32_t)strtoul(v, nullptr, 10);
+        if (K >= 2 && K <= acs_sim::kMaxX && s->rows_per % ((uint64_t)K * bin_sa) == 0) s->xchunks = K;
+    }
+    s->bin_sa = bin_sa;
+    if (s->xchunks) {
+        hipError_t e = hipStreamCreateWithFlags(&s->cstream, hipStreamNonBlocking);
+        for (uint32_t k = 0; e == hipSuccess && k < s->xchunks; ++k) {
+            e = hipEventCreateWithFlags(&s->ev_b[k], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&s->ev_x[k], hipEventDisableTiming);
+        }
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&s->ev_fin, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            fail(ACS_EDEVICE, "comm stream / events: %s", hipGetErrorString(e));
+            release(s);
+            return ACS_EDEVICE;
+        }
+        s->kname += " xchunks" + std::to_string(s->xchunks);
+    }
     if (comm_id) {
         ncclUniqueId id;
         memcpy(&id, comm_id, sizeof id);

@@ -55,6 +55,9 @@ struct RoundArgs {
     // slice actually uses (SELL-64: groups past it are never loaded).  nullptr otherwise.
     const uint8_t* deg;
     const uint8_t* sw;
+    // binned phase B: receiver-block range of this launch, [qlo, qhi) (chunked partitioned rounds
+    // exchange finished chunks while later ones compute); 0, ~0u = every block
+    uint32_t qlo, qhi;
 };
 
 constexpr uint32_t kEllNone = 0xFFFFFFFFu;   // padding column of a CSR row below the compiled degree
@@ -160,8 +163,16 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
 void binned_free(BinnedPlan& p);
 // clean: no slot-dependent decision (selects the plain phase-B instantiation)
 // fin: the previous round's finalize, deferred into this round's phase A (nullptr: none pending)
+// Source-block selection of a phase-A launch (chunked partitioned rounds): with
+// n > 0 only the n blocks a = (u / bpc) * bpr + k0 + u % bpc, u < n, run (chunk k of every rank:
+// bpr blocks per rank, bpc per chunk, k0 = k * bpc); n = 0 runs every block.
+struct SrcSel {
+    uint32_t n, bpr, bpc, k0;
+};
+// Which phases one launch_round_binned call enqueues: 1 = [tag +] scatter (A), 2 = regroup (M),
+// 4 = gather (B, over a.qlo .. a.qhi).
 hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool clean, hipStream_t s,
-                               const FinalizeArgs* fin = nullptr);
+                               const FinalizeArgs* fin = nullptr, uint32_t phases = 7, SrcSel sel = SrcSel{});
 
 // Generic kernel: one workgroup per receiver, LDS bitonic sort (any topology, m <= 8192).
 constexpr uint32_t kGenericMaxM = 8192;

@@ -137,7 +137,7 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
                                                      const uint64_t* __restrict__ aoff, VT* __restrict__ stage,
                                                      const InstState* __restrict__ st, uint64_t N, uint32_t SA,
                                                      uint32_t segs, uint32_t chunk, uint32_t pol,
-                                                     const FinalizeArgs fin, uint32_t fin_on) {
+                                                     const FinalizeArgs fin, uint32_t fin_on, const SrcSel sel) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lx_raw[];
     VT* lx = reinterpret_cast<VT*>(lx_raw);
     if (st->done) return;
@@ -145,10 +145,12 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
     // block a runs on the XCD of blockIdx % 8 = a % 8, so its x block is fetched into one L2 once
     // instead of once per XCD.  The grid is 8 * ceil(P / 8) * segs.
     const uint32_t slot = blockIdx.x >> 3;
-    const uint32_t a = (slot / segs) * 8 + (blockIdx.x & 7u), sg = slot % segs;
+    const uint32_t u = (slot / segs) * 8 + (blockIdx.x & 7u), sg = slot % segs;
+    // selected source blocks (chunked partitioned rounds): launch-local block u -> global block a
+    const uint32_t a = sel.n ? (u < sel.n ? (u / sel.bpc) * sel.bpr + sel.k0 + u % sel.bpc : 0xFFFFFFFFu) : u;
     // padding past the last source block, or a segment past its block's deliveries: idle (but
     // workgroup 0 still records a deferred finalize)
-    const bool idle = (uint64_t)a * SA >= N || aoff[a] + (uint64_t)sg * chunk >= aoff[a + 1];
+    const bool idle = a == 0xFFFFFFFFu || (uint64_t)a * SA >= N || aoff[a] + (uint64_t)sg * chunk >= aoff[a + 1];
     if (idle && !(fin_on && blockIdx.x == 0)) return;
     const uint64_t pa1 = idle ? 0 : aoff[a + 1];
     const uint64_t p0 = idle ? 0 : aoff[a] + (uint64_t)sg * chunk;
@@ -262,7 +264,8 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
     if (S->done) return;
     // XCD-aware order: consecutive receiver blocks (which share the lines at their tile-run
     // seams) run on the same XCD (dispatch is round-robin over the 8 XCDs by blockIdx)
-    const uint32_t b = (blockIdx.x & 7u) * Qc + ((pol & kPolRevB) ? Qc - 1 - (blockIdx.x >> 3) : (blockIdx.x >> 3));
+    const uint32_t b = a.qlo + (blockIdx.x & 7u) * Qc + ((pol & kPolRevB) ? Qc - 1 - (blockIdx.x >> 3) : (blockIdx.x >> 3));
+    if (b >= a.qhi) return;   // past this launch's block range
     if (b >= Q) {   // partial slots past this partition's blocks: neutral (the finalize folds a.nblk)
         if (b < a.nblk && threadIdx.x == 0) a.partial[b] = make_double2(kInf, -kInf);
         return;
@@ -437,7 +440,8 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather_of(const RoundArgs a, con
     __shared__ uint32_t cnt[kBinSB + 64];                                      // + one dummy counter per lane
     InstState* S = a.st;
     if (S->done) return;
-    const uint32_t b = (blockIdx.x & 7u) * Qc + (blockIdx.x >> 3);   // XCD-aware, as k_bin_gather
+    const uint32_t b = a.qlo + (blockIdx.x & 7u) * Qc + (blockIdx.x >> 3);   // XCD-aware, as k_bin_gather
+    if (b >= a.qhi) return;
     if (b >= Q) {
         if (b < a.nblk && threadIdx.x == 0) a.partial[b] = make_double2(kInf, -kInf);
         return;
@@ -1105,32 +1109,42 @@ static hipError_t binned_set_lds_attributes() {
                                p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                  \
     }
 
-hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool clean, hipStream_t s,
-                               const FinalizeArgs* fin) {
+hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool clean, hipStream_t s,
+                               const FinalizeArgs* fin, uint32_t phases, SrcSel sel) {
     const FinalizeArgs fa = fin ? *fin : FinalizeArgs{};
     const uint32_t fin_on = fin ? 1u : 0u;
     const uint32_t pol = p.pol;
     if (hipError_t e = binned_set_lds_attributes(); e != hipSuccess) return e;
+    const uint32_t nsrc = sel.n ? sel.n : p.P;
+    // phase B block range: every partial slot by default (blocks past the plan's Q write neutral
+    // partials), or the caller's [qlo, qhi)
+    RoundArgs a = a0;
+    const uint32_t nslot_all = a.nblk > p.Q ? a.nblk : p.Q;
+    if (a.qhi > nslot_all) a.qhi = nslot_all;
+    if (a.qlo >= a.qhi) phases &= ~4u;
     if (p.f32) {   // fp32 plans: one or two levels; tagged senders need N <= 2^20
         float* st1 = reinterpret_cast<float*>(p.stage1);
         const float* fsrc = reinterpret_cast<const float*>(a.xin);
         if (!clean && a.status) {
             if (!p.xtag || a.N > (1ull << 20)) return hipErrorInvalidValue;
             float* xt = reinterpret_cast<float*>(p.xtag);
-            hipLaunchKernelGGL(k_bin_tag<float>, dim3((unsigned)((a.N + 511) / 512)), dim3(256), 0, s, fsrc, a.status,
-                               xt, a.N, a.r, a.st);
+            if (phases & 1)
+                hipLaunchKernelGGL(k_bin_tag<float>, dim3((unsigned)((a.N + 511) / 512)), dim3(256), 0, s, fsrc, a.status,
+                                   xt, a.N, a.r, a.st);
             fsrc = xt;
         }
-        hipLaunchKernelGGL(k_bin_scatter<float>, dim3((p.P + 7) / 8 * 8 * p.segs), dim3(kBinA), p.SA * sizeof(float), s,
-                           fsrc, p.idxA, p.aoff, st1, a.st, a.N, p.SA, p.segs, p.chunk, pol, fa, fin_on);
+        if (phases & 1)
+            hipLaunchKernelGGL(k_bin_scatter<float>, dim3((nsrc + 7) / 8 * 8 * p.segs), dim3(kBinA), p.SA * sizeof(float), s,
+                               fsrc, p.idxA, p.aoff, st1, a.st, a.N, p.SA, p.segs, p.chunk, pol, fa, fin_on, sel);
         if (p.levels == 2) {
             float* st2 = reinterpret_cast<float*>(p.stage2);
-            hipLaunchKernelGGL(k_bin_regroup<float>, dim3(p.ngroups), dim3(kBinA), (p.mcap + 4) * sizeof(float), s, st1,
-                               p.mt, p.moff, p.idxM, st2, a.st, p.PK, pol);
+            if (phases & 2)
+                hipLaunchKernelGGL(k_bin_regroup<float>, dim3(p.ngroups), dim3(kBinA), (p.mcap + 4) * sizeof(float), s, st1,
+                                   p.mt, p.moff, p.idxM, st2, a.st, p.PK, pol);
             st1 = st2;   // phase B reads the regrouped stage
         }
-        const uint32_t nslot = a.nblk > p.Q ? a.nblk : p.Q;
-        const uint32_t Qc = (nslot + 7) / 8;
+        if (!(phases & 4)) return hipGetLastError();
+        const uint32_t Qc = (a.qhi - a.qlo + 7) / 8;
         const dim3 grid(8 * Qc);
 #define X(DD, TT)                                                                                        \
     if (p.D == DD && a.trim == TT) {                                                                     \
@@ -1165,23 +1179,26 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
     const double* src = a.xin;
     if (!clean && a.status) {
         if (!p.xtag) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_bin_tag<double>, dim3((unsigned)((a.N + 511) / 512)), dim3(256), 0, s, a.xin, a.status, p.xtag,
-                           a.N, a.r, a.st);
+        if (phases & 1)
+            hipLaunchKernelGGL(k_bin_tag<double>, dim3((unsigned)((a.N + 511) / 512)), dim3(256), 0, s, a.xin, a.status,
+                               p.xtag, a.N, a.r, a.st);
         src = p.xtag;
     }
-    hipLaunchKernelGGL(k_bin_scatter<double>, dim3((p.P + 7) / 8 * 8 * p.segs), dim3(kBinA), p.SA * sizeof(double), s, src, p.idxA, p.aoff,
-                       p.stage1, a.st, a.N, p.SA, p.segs, p.chunk, pol, fa, fin_on);
+    if (phases & 1)
+        hipLaunchKernelGGL(k_bin_scatter<double>, dim3((nsrc + 7) / 8 * 8 * p.segs), dim3(kBinA), p.SA * sizeof(double), s, src,
+                           p.idxA, p.aoff, p.stage1, a.st, a.N, p.SA, p.segs, p.chunk, pol, fa, fin_on, sel);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const double* last = p.stage1;
     if (p.levels == 2) {
-        hipLaunchKernelGGL(k_bin_regroup<double>, dim3(p.ngroups), dim3(kBinA), (p.mcap + 2) * sizeof(double), s, p.stage1,
-                           p.mt, p.moff, p.idxM, p.stage2, a.st, p.PK, pol);
+        if (phases & 2)
+            hipLaunchKernelGGL(k_bin_regroup<double>, dim3(p.ngroups), dim3(kBinA), (p.mcap + 2) * sizeof(double), s,
+                               p.stage1, p.mt, p.moff, p.idxM, p.stage2, a.st, p.PK, pol);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         last = p.stage2;
     }
-    const uint32_t nslot = a.nblk > p.Q ? a.nblk : p.Q;
-    const uint32_t Qc = (nslot + 7) / 8;
+    if (!(phases & 4)) return hipGetLastError();
+    const uint32_t Qc = (a.qhi - a.qlo + 7) / 8;
     const dim3 grid(8 * Qc);
 #define X(DD, TT)                                                                                        \
     if (p.D == DD && a.trim == TT) {                                                                     \
