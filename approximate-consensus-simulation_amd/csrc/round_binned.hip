@@ -50,7 +50,9 @@ constexpr uint32_t kPolNtStore = 2;    // phase A / M: nontemporal stage stores
 constexpr uint32_t kPolNtInv = 4;      // phase B: nontemporal invpos loads
 constexpr uint32_t kPolRevB = 8;       // phase B: each XCD walks its receiver-block range downwards
                                        // (the stage tiles phase A wrote last are read first)
-constexpr uint32_t kPolDefault = kPolNtStore | kPolNtInv;   // measured: phase B 80 -> 71 us, phase A -1 us (cfg4)
+constexpr uint32_t kPolNoPf = 16;       // phase B (NP > 1): per-part descriptor loads instead of the prefetch
+constexpr uint32_t kPolBfPick = 32;     // phase B (NP > 1): branch-free pick-up (clamped read + select)
+constexpr uint32_t kPolDefault = kPolNtStore | kPolNtInv | kPolBfPick;   // measured: phase B 80 -> 71 -> 63.2 us (cfg4)   // measured: phase B 80 -> 71 us, phase A -1 us (cfg4)
 
 // ------------------------------------------------------------------------------ shared pieces
 // Stream [p0, p1) of an index stream: out[p] = lds[idx[p]].  Super-steps of 512 positions per
@@ -128,6 +130,26 @@ __device__ __forceinline__ void bin_dma_runs(const uint2* __restrict__ tb, uint3
                     if (o + lane < n16) __builtin_amdgcn_global_load_lds(sp + o, dp + o, 16, 0, 0);
             }
         }
+    }
+}
+
+// The same copy for runs [r0, r1) of a block of at most 64 runs whose descriptors the wave already
+// holds one per lane (dsc = tb[lane], nxt = tb[lane + 1].y): no load before the first DMA.
+template <typename VT = double>
+__device__ __forceinline__ void bin_dma_runs_pf(uint2 dsc, uint32_t nxt, uint32_t r0, uint32_t r1,
+                                                const VT* __restrict__ src, VT* dst, uint32_t base) {
+    constexpr uint32_t EPU = 16 / sizeof(VT);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint4* s16 = reinterpret_cast<const uint4*>(src);
+    uint4* d16 = reinterpret_cast<uint4*>(dst);
+    for (uint32_t k = r0; k < r1; ++k) {
+        const uint32_t so = __builtin_amdgcn_readlane(dsc.x, k);
+        const uint32_t pre = __builtin_amdgcn_readlane(dsc.y, k);
+        const uint32_t n16 = (__builtin_amdgcn_readlane(nxt, k) - pre) / EPU;
+        const uint4* sp = s16 + so / EPU + lane;
+        uint4* dp = d16 + (pre - base) / EPU;
+        for (uint32_t o = 0; o < n16; o += 64)
+            if (o + lane < n16) __builtin_amdgcn_global_load_lds(sp + o, dp + o, 16, 0, 0);
     }
 }
 
@@ -275,7 +297,23 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
     const uint64_t li = (uint64_t)b * kBinSB + threadIdx.x;   // local row
     const uint64_t i = a.row0 + li;                              // global receiver
     const bool live = li < a.nrows;
-    // ordinary loads first (their wait is the barrier's vmcnt(0) anyway)
+    const uint2* tb = tiles + (uint64_t)b * (nrun + 1);
+    // NP-pass blocks of at most 64 runs: every wave fetches all descriptors first (one per lane)
+    // and issues part 0's DMA before anything else is in flight, so the only wait ahead of the
+    // first transfer is the descriptor load itself; later parts issue from registers.
+    const bool pf = NP > 1 && nrun <= 64 && !(pol & kPolNoPf);
+    uint2 pdsc = make_uint2(0u, 0u);
+    uint32_t pnxt = 0;
+    if (pf) {
+        const uint32_t lane = threadIdx.x & 63;
+        if (lane < nrun) {
+            pdsc = tb[lane];
+            pnxt = tb[lane + 1].y;
+        }
+        const uint32_t j1 = nrun / NP;
+        bin_dma_runs_pf(pdsc, pnxt, w * j1 / NW, (w + 1) * j1 / NW, stage, raw, 0u);
+    }
+    // ordinary loads next (their wait is the barrier's vmcnt(0) anyway)
     const VT xi = live ? reinterpret_cast<const VT*>(a.xin)[i] : VT(0);
     uint32_t si = kHonest;
     if constexpr (FAULTY) {
@@ -303,7 +341,6 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
 #pragma unroll
         for (int q = 0; q < D / 8; ++q) ip[q] = ipp[q * kBinSB];
     }
-    const uint2* tb = tiles + (uint64_t)b * (nrun + 1);
     VT v[D + 1];
     if constexpr (NP == 1) {
         bin_dma_runs(tb, w * nrun / NW, (w + 1) * nrun / NW, stage, raw, (pol & kPolNtRuns) != 0);
@@ -325,10 +362,21 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
         // a ragged last block alike — is below tb[nrun].y (hi of the last part).
         for (uint32_t k = 0; k < (uint32_t)NP; ++k) {
             const uint32_t j0 = k * nrun / NP, j1 = (k + 1) * nrun / NP;
-            const uint32_t lo = tb[j0].y, hi = tb[j1].y;   // image range of this part (pad-unit aligned)
+            uint32_t lo, hi;   // image range of this part (pad-unit aligned)
+            if (pf) {
+                lo = __builtin_amdgcn_readlane(pdsc.y, j0);
+                hi = j1 < nrun ? __builtin_amdgcn_readlane(pdsc.y, j1) : __builtin_amdgcn_readlane(pnxt, nrun - 1);
+            } else {
+                lo = tb[j0].y;
+                hi = tb[j1].y;
+            }
             if (k) __syncthreads();   // every lane has read the previous part before it is overwritten
-            bin_dma_runs(tb, j0 + w * (j1 - j0) / NW, j0 + (w + 1) * (j1 - j0) / NW, stage, raw,
-                         (pol & kPolNtRuns) != 0, lo);
+            if (pf) {
+                if (k) bin_dma_runs_pf(pdsc, pnxt, j0 + w * (j1 - j0) / NW, j0 + (w + 1) * (j1 - j0) / NW, stage, raw, lo);
+            } else {
+                bin_dma_runs(tb, j0 + w * (j1 - j0) / NW, j0 + (w + 1) * (j1 - j0) / NW, stage, raw,
+                             (pol & kPolNtRuns) != 0, lo);
+            }
             __syncthreads();
 #pragma unroll
             for (int q = 0; q < D / 8; ++q) {
@@ -336,8 +384,16 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const uint32_t p0 = wd[e] & 0xFFFFu, p1 = wd[e] >> 16;
-                    if ((k == 0 || p0 >= lo) && (k + 1 == (uint32_t)NP || p0 < hi)) v[1 + 8 * q + 2 * e] = raw[p0 - lo];
-                    if ((k == 0 || p1 >= lo) && (k + 1 == (uint32_t)NP || p1 < hi)) v[2 + 8 * q + 2 * e] = raw[p1 - lo];
+                    const bool in0 = (k == 0 || p0 >= lo) && (k + 1 == (uint32_t)NP || p0 < hi);
+                    const bool in1 = (k == 0 || p1 >= lo) && (k + 1 == (uint32_t)NP || p1 < hi);
+                    if (pol & kPolBfPick) {   // every lane reads (offset 0 when out of this part), then selects
+                        const VT t0 = raw[in0 ? p0 - lo : 0u], t1 = raw[in1 ? p1 - lo : 0u];
+                        v[1 + 8 * q + 2 * e] = in0 ? t0 : v[1 + 8 * q + 2 * e];
+                        v[2 + 8 * q + 2 * e] = in1 ? t1 : v[2 + 8 * q + 2 * e];
+                    } else {
+                        if (in0) v[1 + 8 * q + 2 * e] = raw[p0 - lo];
+                        if (in1) v[2 + 8 * q + 2 * e] = raw[p1 - lo];
+                    }
                 }
             }
         }
@@ -988,7 +1044,7 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     p.ofree = ofree;
     {
         const char* v = getenv("ACSIM_BIN_POL");
-        p.pol = v ? (uint32_t)strtoul(v, nullptr, 0) & 15u : kPolDefault;
+        p.pol = v ? (uint32_t)strtoul(v, nullptr, 0) & 63u : kPolDefault;
     }
     if (ofree) {   // order-free phase B: receiver ids in image order
         p.rstride = ((uint32_t)d * kBinSB + p.nrun * (G.pad - 1) + 15u) & ~15u;
