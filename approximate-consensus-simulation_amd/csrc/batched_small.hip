@@ -65,6 +65,8 @@ struct LaneCtx {
     uint32_t N, lane, b, r;
     VT xi, lo, hi;
     uint32_t sti;
+    const VT* xs;          // this round's x of every node of the instance (LDS, broadcast reads)
+    const uint32_t* ss;    // every node's status word (LDS)
     uint64_t miss;   // bit j: message from j missing (crash or drop)
     VT fill;         // missing_policy = OMIT: the value a missing entry takes (omit_fill)
 };
@@ -80,13 +82,16 @@ __device__ __noinline__ VT byz_value_ool(const MsgParams& mp, uint32_t b, uint32
 
 // §A.6 entry j of receiver `lane` (valid for j < N).  FAULTS = false: no fault schedule, so a
 // sender is never Byzantine and only the drop bits matter (cfg3).
+// Sender values come from an LDS copy of the instance's x (a wave-uniform address: one broadcast
+// read per entry) rather than v_readlane: 64 readlane pairs per round held 128 SGPRs live, which
+// spilled to VGPR lanes and cost more VALU than the Philox draws.
 template <bool FAULTS, typename VT>
 __device__ __forceinline__ VT entry_value(const LaneCtx<VT>& c, int j) {
-    const VT xj = readlane_v(c.xi, j);
+    const VT xj = c.xs[j];
     if ((uint32_t)j == c.lane) return c.xi;
     if ((c.miss >> j) & 1ull) return c.mp->omit ? c.fill : c.xi;   // OMIT: +0.0 / +inf
     if constexpr (FAULTS) {
-        const uint32_t stj = (uint32_t)__builtin_amdgcn_readlane((int)c.sti, j);
+        const uint32_t stj = c.ss[j];
         if (stj == kByz) return byz_value_ool(*c.mp, c.b, c.r, c.lane, (uint64_t)c.lane * c.N + j, c.lo, c.hi);
     }
     return xj;
@@ -97,6 +102,45 @@ __device__ __forceinline__ VT average_tree(const LaneCtx<VT>& c, std::integer_se
     constexpr int LOG2P = ilog2(P);
     VT acc[LOG2P + 1];
     (push_leaf<P, Q, LOG2P>(acc, (bitrev<LOG2P>(Q) < (int)c.N) ? entry_value<FAULTS>(c, bitrev<LOG2P>(Q)) : VT(0)), ...);
+    return acc[LOG2P];
+}
+
+// Bit-select of two values of the same width: (m & a) | (~m & b) per 32-bit word (v_bfi_b32), m all
+// ones or all zeros.  No lane-mask (SGPR pair) per entry: 64 entries' compare masks held live
+// otherwise spill SGPRs to VGPR lanes.
+__device__ __forceinline__ double bitsel(uint32_t m, double a, double b) {
+    const uint64_t ua = (uint64_t)__double_as_longlong(a), ub = (uint64_t)__double_as_longlong(b);
+    const uint32_t lo = (m & (uint32_t)ua) | (~m & (uint32_t)ub);
+    const uint32_t hi = (m & (uint32_t)(ua >> 32)) | (~m & (uint32_t)(ub >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ float bitsel(uint32_t m, float a, float b) {
+    return __uint_as_float((m & __float_as_uint(a)) | (~m & __float_as_uint(b)));
+}
+
+// AVERAGE without a fault schedule (cfg3): entry j is x_i when bit j of `usexi` is set (missing
+// messages under §A.6 substitution), +0.0 when bit j of `use0` is set (missing messages under
+// OMIT), else x_j from the LDS copy — which for j = lane IS x_i, so the self entry
+// needs no lane-dependent test (use0 never holds the self bit).  FULL: N == P (no padding test).
+template <int P, bool OMIT, bool FULL, typename VT, int... Q>
+__device__ __forceinline__ VT average_tree_sel(const VT* xs, VT xi, uint64_t usexi, uint64_t use0, uint32_t N,
+                                               std::integer_sequence<int, Q...>) {
+    constexpr int LOG2P = ilog2(P);
+    VT acc[LOG2P + 1];
+    const uint32_t w0 = (uint32_t)usexi, w1 = (uint32_t)(usexi >> 32);
+    const uint32_t z0 = (uint32_t)use0, z1 = (uint32_t)(use0 >> 32);
+    auto leaf = [&](int j) -> VT {
+        if (!FULL && j >= (int)N) return VT(0);
+        VT v = xs[j];
+        if constexpr (OMIT) v = bitsel(0u - (((j < 32 ? z0 : z1) >> (j & 31)) & 1u), VT(0), v);
+        return bitsel(0u - (((j < 32 ? w0 : w1) >> (j & 31)) & 1u), xi, v);
+    };
+    // scheduling fence every 8 leaves: unfenced, the compiler hoists all 64 LDS reads (128 VGPRs
+    // live, one wave per SIMD); fenced, a group's reads overlap only the previous group's adds
+    auto fence = [](int q) {
+        if ((q & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+    };
+    ((push_leaf<P, Q, LOG2P>(acc, leaf(bitrev<LOG2P>(Q))), fence(Q)), ...);
     return acc[LOG2P];
 }
 
@@ -120,12 +164,20 @@ __global__ __launch_bounds__(64) void k_batched_small(const BatchArgs a, uint32_
     const uint32_t sti = valid ? (a.status ? a.status[(uint64_t)lb * N + lane] : kHonest) : kByz;
     const bool honest = sti == kHonest;
     __shared__ VT colbuf[SORT ? P * 64 : 1];
+    __shared__ VT xs[64];
+    __shared__ uint32_t ss[64];
+    ss[lane] = sti;   // read after the first round's barrier
     bool done = false, conv = spread <= a.eps;
     for (uint32_t q = 0; q < kmax; ++q) {
         const bool act = valid && is_active(sti, r);
         LaneCtx<VT> c;
         c.mp = &mp; c.N = N; c.lane = lane; c.b = b; c.r = r; c.xi = xi; c.lo = (VT)lo; c.hi = (VT)hi;
         c.sti = sti;
+        __syncthreads();   // (one wave: orders the previous round's reads before this write)
+        xs[lane] = xi;
+        __syncthreads();
+        c.xs = xs;
+        c.ss = ss;
         c.miss = 0;
         // drop mask (§A.5): slot s = lane*N + j
         if (mp.thr && act) {
@@ -156,7 +208,17 @@ __global__ __launch_bounds__(64) void k_batched_small(const BatchArgs a, uint32_
         const uint32_t mn_ = mp.omit ? N - (uint32_t)__builtin_popcountll(c.miss) : N;
         VT res;
         if constexpr (!SORT) {
-            res = average_tree<P, FAULTS>(c, std::make_integer_sequence<int, P>{}) / (VT)mn_;
+            if constexpr (!FAULTS) {
+                constexpr auto seq = std::make_integer_sequence<int, P>{};
+                if (mp.omit)
+                    res = (N == P ? average_tree_sel<P, true, true>(xs, xi, 0ull, c.miss, N, seq)
+                                  : average_tree_sel<P, true, false>(xs, xi, 0ull, c.miss, N, seq)) / (VT)mn_;
+                else
+                    res = (N == P ? average_tree_sel<P, false, true>(xs, xi, c.miss, 0ull, N, seq)
+                                  : average_tree_sel<P, false, false>(xs, xi, c.miss, 0ull, N, seq)) / (VT)mn_;
+            } else {
+                res = average_tree<P, FAULTS>(c, std::make_integer_sequence<int, P>{}) / (VT)mn_;
+            }
         } else {
             VT v[P];
 #pragma unroll

@@ -52,7 +52,7 @@ constexpr uint32_t kPolRevB = 8;       // phase B: each XCD walks its receiver-b
                                        // (the stage tiles phase A wrote last are read first)
 constexpr uint32_t kPolNoPf = 16;       // phase B (NP > 1): per-part descriptor loads instead of the prefetch
 constexpr uint32_t kPolBfPick = 32;     // phase B (NP > 1): branch-free pick-up (clamped read + select)
-constexpr uint32_t kPolDefault = kPolNtStore | kPolNtInv | kPolBfPick;   // measured: phase B 80 -> 71 -> 63.2 us (cfg4)   // measured: phase B 80 -> 71 us, phase A -1 us (cfg4)
+constexpr uint32_t kPolDefault = kPolNtStore | kPolNtInv | kPolBfPick;   // measured (cfg4): phase B 80 -> 71 (nt) -> 63.2 us (pick-up), phase A -1 us
 
 // ------------------------------------------------------------------------------ shared pieces
 // Stream [p0, p1) of an index stream: out[p] = lds[idx[p]].  Super-steps of 512 positions per
