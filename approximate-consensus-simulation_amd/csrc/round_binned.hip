@@ -58,8 +58,24 @@ constexpr uint32_t kPolDefault = kPolNtStore | kPolNtInv | kPolBfPick;   // meas
 // Stream [p0, p1) of an index stream: out[p] = lds[idx[p]].  Super-steps of 512 positions per
 // wave; instruction q of a lane covers positions q*128 + 2*lane, +1 (one u32 of two indices, one
 // 16-byte store), so every wave-instruction reads 256 B and writes 1 KiB contiguously.
+// Software-pipelined by batches of SB super-steps: the index loads of batch k+1 are issued before
+// batch k's gathers and stores.  (gfx9 counts loads and stores in one in-order vmcnt: the plain
+// loop's wait for its index loads also waited for the previous batch's store completions, so each
+// batch paid a full store round trip.)
 __device__ __forceinline__ double2 bin_pair(double a, double b) { return make_double2(a, b); }
 __device__ __forceinline__ float2 bin_pair(float a, float b) { return make_float2(a, b); }
+
+template <typename V2>
+__device__ __forceinline__ void bin_store(V2* dst, const V2& v, bool nt) {
+    if (nt) {   // as an integer vector of V2's size (the builtin takes native vector types)
+        using UV = unsigned int __attribute__((ext_vector_type(sizeof(V2) / 4)));
+        UV bits;
+        __builtin_memcpy(&bits, &v, sizeof(V2));
+        __builtin_nontemporal_store(bits, reinterpret_cast<UV*>(dst));
+    } else {
+        *dst = v;
+    }
+}
 
 // VT = double, or float for fp32 plans (the instruction's store is then 8 bytes)
 template <typename VT = double>
@@ -67,28 +83,47 @@ __device__ __forceinline__ void bin_stream(const VT* lx, const uint16_t* __restr
                                            uint64_t p0, uint64_t p1, bool nt_store = false) {
     using V2 = decltype(bin_pair(VT(0), VT(0)));
     constexpr uint32_t SUP = kBinA / 64 * 512, SUPW = SUP / 2;
+    constexpr uint32_t SB = 1;   // super-steps per pipelined batch
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint64_t p = p0;
     if ((p0 & 1) == 0) {
         const uint64_t nsup = (p1 - p0) / SUP;
+        const uint64_t nb = nsup / SB;
         const uint32_t* ip = reinterpret_cast<const uint32_t*>(idx + p0) + w * 256 + lane;
         V2* op = reinterpret_cast<V2*>(out + p0) + w * 256 + lane;
-#pragma unroll 4
-        for (uint64_t k = 0; k < nsup; ++k) {
-            uint32_t c[4];
+        uint32_t c[SB][4];
+        if (nb) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) c[q] = __builtin_nontemporal_load(ip + k * SUPW + q * 64);
+            for (uint32_t u = 0; u < SB; ++u)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const V2 v = bin_pair(lx[c[q] & 0xFFFFu], lx[c[q] >> 16]);
-                if (nt_store) {   // as an integer vector of V2's size (the builtin takes native vector types)
-                    using UV = unsigned int __attribute__((ext_vector_type(sizeof(V2) / 4)));
-                    UV bits;
-                    __builtin_memcpy(&bits, &v, sizeof(V2));
-                    __builtin_nontemporal_store(bits, reinterpret_cast<UV*>(op + k * SUPW + q * 64));
-                } else
-                    op[k * SUPW + q * 64] = v;
-            }
+                for (int q = 0; q < 4; ++q) c[u][q] = __builtin_nontemporal_load(ip + u * SUPW + q * 64);
+        }
+        for (uint64_t bi = 0; bi < nb; ++bi) {
+            // next batch's indices (the last batch re-reads itself: no branch around the loads)
+            const uint64_t bn = bi + 1 < nb ? bi + 1 : bi;
+            uint32_t cn[SB][4];
+#pragma unroll
+            for (uint32_t u = 0; u < SB; ++u)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) cn[u][q] = __builtin_nontemporal_load(ip + (bn * SB + u) * SUPW + q * 64);
+#pragma unroll
+            for (uint32_t u = 0; u < SB; ++u)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    bin_store(op + (bi * SB + u) * SUPW + q * 64, bin_pair(lx[c[u][q] & 0xFFFFu], lx[c[u][q] >> 16]),
+                              nt_store);
+#pragma unroll
+            for (uint32_t u = 0; u < SB; ++u)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) c[u][q] = cn[u][q];
+        }
+        for (uint64_t k = nb * SB; k < nsup; ++k) {   // the last < SB super-steps
+            uint32_t cc[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cc[q] = __builtin_nontemporal_load(ip + k * SUPW + q * 64);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                bin_store(op + k * SUPW + q * 64, bin_pair(lx[cc[q] & 0xFFFFu], lx[cc[q] >> 16]), nt_store);
         }
         p = p0 + nsup * SUP;
     }
