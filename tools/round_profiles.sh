@@ -12,10 +12,10 @@ timeout -k 10 300 python3 "$B" > "$out/bench_f64.json" 2> "$out/bench_f64.err" |
 timeout -k 10 300 python3 "$B" --dtype f32 > "$out/bench_f32.json" 2> "$out/bench_f32.err" || exit $?
 for dt in f64 f32; do
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/stats_$dt" -o run -- \
-      python3 "$B" --no-cpu-baseline --dtype $dt > "$out/stats_$dt.log" 2>&1 || exit $?
+      python3 "$B" --no-cpu-baseline --legs= --dtype $dt > "$out/stats_$dt.log" 2>&1 || exit $?
   for pass in "FETCH_SIZE" "WRITE_SIZE"; do
     timeout -s KILL 120 rocprofv3 --pmc $pass --output-format csv -d "$out/pmc_${dt}_$pass" -o run -- \
-        python3 "$B" --no-cpu-baseline --dtype $dt --steps 30 > "$out/pmc_${dt}_$pass.log" 2>&1 || exit $?
+        python3 "$B" --no-cpu-baseline --legs= --dtype $dt --steps 30 > "$out/pmc_${dt}_$pass.log" 2>&1 || exit $?
   done
 done
 echo done
