@@ -58,6 +58,7 @@ struct RoundArgs {
     // binned phase B: receiver-block range of this launch, [qlo, qhi) (chunked partitioned rounds
     // exchange finished chunks while later ones compute); 0, ~0u = every block
     uint32_t qlo, qhi;
+    uint64_t* ts;             // diagnostic per-workgroup timestamps (ACSIM_BIN_TS; nullptr otherwise)
 };
 
 constexpr uint32_t kEllNone = 0xFFFFFFFFu;   // padding column of a CSR row below the compiled degree
@@ -151,6 +152,8 @@ struct BinnedPlan {
     double* stage1 = nullptr;           // [Ep1]
     double* stage2 = nullptr;           // [Ep2] (two levels)
     double* xtag = nullptr;             // [N+2] tagged sender values (fault schedules only)
+    uint64_t* ts = nullptr;             // ACSIM_BIN_TS=<file>: [3 * (ts_a + ts_b)] workgroup timestamps of the last round
+    uint32_t ts_a = 0, ts_b = 0;        // phase-A / phase-B workgroups recorded
 };
 bool binned_supported(uint32_t d, uint32_t t, uint32_t rule);
 // 1 or 2 exchange levels for NR local receivers of an N-node graph (0: not supported).

@@ -191,16 +191,29 @@ __device__ __forceinline__ void bin_dma_runs_pf(uint2 dsc, uint32_t nxt, uint32_
     }
 }
 
+// diagnostic (ACSIM_BIN_TS): workgroup entry, end of its staging wait, end, in 100 MHz ticks
+__device__ __forceinline__ void bin_ts(uint64_t* ts, uint64_t t0, uint64_t t1) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
+        ts[3 * blockIdx.x] = t0;
+        ts[3 * blockIdx.x + 1] = t1;
+        ts[3 * blockIdx.x + 2] = t2;
+    }
+}
+
 // ------------------------------------------------------------------------------ phase A
 template <typename VT = double>
 __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x, const uint16_t* __restrict__ idxA,
                                                      const uint64_t* __restrict__ aoff, VT* __restrict__ stage,
                                                      const InstState* __restrict__ st, uint64_t N, uint32_t SA,
                                                      uint32_t segs, uint32_t chunk, uint32_t pol,
-                                                     const FinalizeArgs fin, uint32_t fin_on, const SrcSel sel) {
+                                                     const FinalizeArgs fin, uint32_t fin_on, const SrcSel sel,
+                                                     uint64_t* __restrict__ ts) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lx_raw[];
     VT* lx = reinterpret_cast<VT*>(lx_raw);
     if (st->done) return;
+    const uint64_t t0 = ts ? __builtin_amdgcn_s_memrealtime() : 0;
     // XCD-aware order (dispatch deals blocks round-robin over the 8 XCDs): every segment of source
     // block a runs on the XCD of blockIdx % 8 = a % 8, so its x block is fetched into one L2 once
     // instead of once per XCD.  The grid is 8 * ceil(P / 8) * segs.
@@ -244,7 +257,9 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
     } else {
         __syncthreads();
     }
+    const uint64_t t1 = ts ? __builtin_amdgcn_s_memrealtime() : 0;
     bin_stream(lx, idxA, stage, p0, p1, (pol & kPolNtStore) != 0);
+    if (ts) bin_ts(ts, t0, t1);
 }
 
 // ------------------------------------------------------------------------------ phase M
@@ -322,6 +337,8 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
     VT raw[NP > 1 ? kBinPartCap<D, NP> : D * kBinSB + D * kBinSB / 16 * (16 / sizeof(VT) - 1)];
     InstState* S = a.st;
     if (S->done) return;
+    const uint64_t t0 = a.ts ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint64_t t1 = 0;
     // XCD-aware order: consecutive receiver blocks (which share the lines at their tile-run
     // seams) run on the same XCD (dispatch is round-robin over the 8 XCDs by blockIdx)
     const uint32_t b = a.qlo + (blockIdx.x & 7u) * Qc + ((pol & kPolRevB) ? Qc - 1 - (blockIdx.x >> 3) : (blockIdx.x >> 3));
@@ -383,6 +400,7 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
     if constexpr (NP == 1) {
         bin_dma_runs(tb, w * nrun / NW, (w + 1) * nrun / NW, stage, raw, (pol & kPolNtRuns) != 0);
         __syncthreads();
+        if (a.ts) t1 = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
         for (int q = 0; q < D / 8; ++q) {
             const uint32_t wd[4] = {ip[q].x, ip[q].y, ip[q].z, ip[q].w};
@@ -416,6 +434,7 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
                              (pol & kPolNtRuns) != 0, lo);
             }
             __syncthreads();
+            if (k == 0 && a.ts) t1 = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
             for (int q = 0; q < D / 8; ++q) {
                 const uint32_t wd[4] = {ip[q].x, ip[q].y, ip[q].z, ip[q].w};
@@ -509,6 +528,7 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
         }
     }
     block_minmax_store<kBinSB>(mn, mx, a.partial + b);
+    if (a.ts) bin_ts(a.ts, t0, t1);
 }
 
 // ------------------------------------------------------------------------------ phase B, order-free
@@ -889,6 +909,20 @@ uint32_t binned_levels(uint64_t N, uint64_t NR, uint32_t d, uint32_t sa, uint32_
 }
 
 void binned_free(BinnedPlan& p) {
+    if (p.ts) {   // diagnostic dump: phase,workgroup,t_entry,t_staged,t_end (100 MHz ticks)
+        std::vector<uint64_t> h(3ull * (p.ts_a + p.ts_b));
+        const char* fn = getenv("ACSIM_BIN_TS");
+        if (fn && hipMemcpy(h.data(), p.ts, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+            if (FILE* f = fopen(fn, "w")) {
+                for (uint64_t k = 0; k < p.ts_a + p.ts_b; ++k)
+                    fprintf(f, "%c,%llu,%llu,%llu,%llu\n", k < p.ts_a ? 'A' : 'B',
+                            (unsigned long long)(k < p.ts_a ? k : k - p.ts_a), (unsigned long long)h[3 * k],
+                            (unsigned long long)h[3 * k + 1], (unsigned long long)h[3 * k + 2]);
+                fclose(f);
+            }
+        }
+        (void)hipFree(p.ts);
+    }
     (void)hipFree(p.idxA);
     (void)hipFree(p.idxM);
     (void)hipFree(p.invpos);
@@ -1157,6 +1191,12 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
         p.segs = (uint32_t)((mx + p.chunk - 1) / p.chunk);
         if (p.segs == 0) p.segs = 1;
     }
+    if (e == hipSuccess && getenv("ACSIM_BIN_TS")) {   // diagnostic workgroup timestamps
+        p.ts_a = (p.P + 7) / 8 * 8 * p.segs;
+        p.ts_b = (p.Q + 7) / 8 * 8;
+        e = hipMalloc(&p.ts, 3ull * (p.ts_a + p.ts_b) * sizeof(uint64_t));
+        if (e == hipSuccess) e = hipMemset(p.ts, 0, 3ull * (p.ts_a + p.ts_b) * sizeof(uint64_t));
+    }
     T1.release();
     T2.release();
     return e;
@@ -1213,6 +1253,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
     // phase B block range: every partial slot by default (blocks past the plan's Q write neutral
     // partials), or the caller's [qlo, qhi)
     RoundArgs a = a0;
+    a.ts = p.ts ? p.ts + 3ull * p.ts_a : nullptr;
     const uint32_t nslot_all = a.nblk > p.Q ? a.nblk : p.Q;
     if (a.qhi > nslot_all) a.qhi = nslot_all;
     if (a.qlo >= a.qhi) phases &= ~4u;
@@ -1229,7 +1270,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
         }
         if (phases & 1)
             hipLaunchKernelGGL(k_bin_scatter<float>, dim3((nsrc + 7) / 8 * 8 * p.segs), dim3(kBinA), p.SA * sizeof(float), s,
-                               fsrc, p.idxA, p.aoff, st1, a.st, a.N, p.SA, p.segs, p.chunk, pol, fa, fin_on, sel);
+                               fsrc, p.idxA, p.aoff, st1, a.st, a.N, p.SA, p.segs, p.chunk, pol, fa, fin_on, sel, p.ts);
         if (p.levels == 2) {
             float* st2 = reinterpret_cast<float*>(p.stage2);
             if (phases & 2)
@@ -1280,7 +1321,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
     }
     if (phases & 1)
         hipLaunchKernelGGL(k_bin_scatter<double>, dim3((nsrc + 7) / 8 * 8 * p.segs), dim3(kBinA), p.SA * sizeof(double), s, src,
-                           p.idxA, p.aoff, p.stage1, a.st, a.N, p.SA, p.segs, p.chunk, pol, fa, fin_on, sel);
+                           p.idxA, p.aoff, p.stage1, a.st, a.N, p.SA, p.segs, p.chunk, pol, fa, fin_on, sel, p.ts);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const double* last = p.stage1;

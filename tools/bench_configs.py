@@ -31,6 +31,10 @@ CASES = {
     # user graph (§8(f) row 1): 2^20 nodes, power-law degrees 11..32, hub-skewed senders, trimmed t=5
     "csr_2e20": dict(max_rounds=20),
     "csr_2e20_generic": dict(max_rounds=20),   # the same graph on the one-workgroup-per-receiver kernel
+    # size probes of the headline shape (stage 64 / 128 / 512 MiB against the 256 MiB MALL)
+    "cfg4_n18": dict(max_rounds=100, n_nodes=1 << 18),
+    "cfg4_n19": dict(max_rounds=100, n_nodes=1 << 19),
+    "cfg4_n21": dict(max_rounds=100, n_nodes=1 << 21),
 }
 
 
@@ -41,7 +45,7 @@ def run(name, **kw):
         csr = skewed_csr(1 << 20, 11, 32, 11)
         cfg = acsim.Config(n_nodes=1 << 20, topology="csr", rule="trimmed", trim=5, termination="fixed", **kw)
         os.environ["ACSIM_CSR_FAST"] = "0" if name.endswith("_generic") else "1"
-    elif name == "cfg4_fixed14":
+    elif name == "cfg4_fixed14" or name.startswith("cfg4_n"):
         cfg = acsim.preset("cfg4", **kw)
     elif name.endswith("_f32"):
         cfg = acsim.preset(name[:-4], dtype="f32", **kw)
