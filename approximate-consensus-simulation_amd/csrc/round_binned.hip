@@ -286,7 +286,7 @@ __global__ __launch_bounds__(kBinA) void k_bin_regroup(const VT* __restrict__ st
 // The runs of block b (run j of a table row of nrun + 1 descriptors) are copied into LDS,
 // concatenated; lane i_local then reads its D values at invpos[b][t][i_local].
 // quiet-NaN tag of a non-normal sender: payload bits 0-1 = 1 Byzantine, 2 crashing this round,
-// 3 silent; bits 2-33 = the sender id (read back for mode 2; B·N < 2^31 with a fault schedule)
+// 3 silent; bits 2-33 = the sender id (read back for mode 2; binned plans hold one instance, N < 2^32)
 constexpr uint64_t kTagBase = 0x7FF8000000000000ull;
 
 // fp32 plans use the binary32 quiet NaN 0x7FC00000 with the same payload layout in

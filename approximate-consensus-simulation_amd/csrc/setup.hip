@@ -1,6 +1,7 @@
 // setup.hip — one-time device setup: initial values, the Feistel
 // graph as an ELL slice layout, and the fault schedule.  Not timed as the hot path, but
 // bit-exact with the spec like everything else.
+#include <cstdlib>
 #include <hipcub/hipcub.hpp>
 
 #include "engine.hpp"
@@ -150,33 +151,48 @@ hipError_t launch_build_ell(uint32_t* ell, uint64_t N, uint64_t row0, uint64_t n
     return hipGetLastError();
 }
 
+// §A.4 fault schedule of B instances.  The segmented radix sort takes int sizes, so instances are
+// processed in batches of nb with nb * N < 2^31 (and at most 2^28 keys, 4 GiB of key buffers);
+// ACSIM_FAULT_BATCH caps nb (tests force several batches on small configs).  Needs N < 2^31.
 hipError_t build_fault_status(uint32_t* status, uint64_t B, uint64_t N, uint32_t f,
                               uint32_t fault_model, uint32_t crash_window, Key key,
                               uint64_t inst_offset, hipStream_t s) {
     hipError_t e;
-    const uint64_t n = B * N;
-    hipLaunchKernelGGL(k_fill_u32, dim3(1024), dim3(256), 0, s, status, n, kHonest);
+    hipLaunchKernelGGL(k_fill_u32, dim3(1024), dim3(256), 0, s, status, B * N, kHonest);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (fault_model == 0 || f == 0) return hipSuccess;
+    if (N >= (1ull << 31)) return hipErrorNotSupported;
+    uint64_t nb = ((1ull << 28) + N - 1) / N;   // instances per batch
+    if (nb * N >= (1ull << 31)) nb = ((1ull << 31) - 1) / N;
+    if (const char* v = getenv("ACSIM_FAULT_BATCH")) {
+        const uint64_t cap = strtoull(v, nullptr, 10);
+        if (cap && cap < nb) nb = cap;
+    }
+    if (nb > B) nb = B;
+    if (nb > 65535) nb = 65535;   // grid y
+    const uint64_t n = nb * N;
     uint64_t *keys = nullptr, *sorted = nullptr;
     void* temp = nullptr;
     size_t temp_bytes = 0;
     if ((e = hipMalloc(&keys, n * sizeof(uint64_t))) != hipSuccess) return e;
     if ((e = hipMalloc(&sorted, n * sizeof(uint64_t))) != hipSuccess) { (void)hipFree(keys); return e; }
-    hipLaunchKernelGGL(k_fault_keys, dim3((unsigned)((N + 255) / 256), (unsigned)B), dim3(256), 0, s, keys, N,
-                       key, inst_offset);
     auto offs = hipcub::TransformInputIterator<uint64_t, SegOffset, hipcub::CountingInputIterator<uint64_t>>(
         hipcub::CountingInputIterator<uint64_t>(0), SegOffset{N});
-    e = hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, temp_bytes, keys, sorted, (int)n, (int)B, offs,
+    e = hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, temp_bytes, keys, sorted, (int)n, (int)nb, offs,
                                                    offs + 1, 0, 64, s);
     if (e == hipSuccess) e = hipMalloc(&temp, temp_bytes ? temp_bytes : 16);
-    if (e == hipSuccess)
-        e = hipcub::DeviceSegmentedRadixSort::SortKeys(temp, temp_bytes, keys, sorted, (int)n, (int)B, offs,
+    for (uint64_t b0 = 0; e == hipSuccess && b0 < B; b0 += nb) {
+        const uint64_t bn = B - b0 < nb ? B - b0 : nb;
+        hipLaunchKernelGGL(k_fault_keys, dim3((unsigned)((N + 255) / 256), (unsigned)bn), dim3(256), 0, s, keys, N,
+                           key, inst_offset + b0);
+        size_t tb = temp_bytes;
+        e = hipcub::DeviceSegmentedRadixSort::SortKeys(temp, tb, keys, sorted, (int)(bn * N), (int)bn, offs,
                                                        offs + 1, 0, 64, s);
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_mark_faults, dim3((f + 255) / 256, (unsigned)B), dim3(256), 0, s, status, sorted,
-                           N, f, fault_model, crash_window, key, inst_offset);
-        e = hipGetLastError();
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_mark_faults, dim3((f + 255) / 256, (unsigned)bn), dim3(256), 0, s, status + b0 * N,
+                               sorted, N, f, fault_model, crash_window, key, inst_offset + b0);
+            e = hipGetLastError();
+        }
     }
     hipError_t e2 = hipStreamSynchronize(s);
     if (e == hipSuccess) e = e2;
