@@ -72,6 +72,8 @@ struct acs_sim {
     bool mfma = false;             // PATH_BATCHED served by the MFMA group kernel (batched_mfma.hip)
     bool dense_persist = false;    // PATH_DENSE served by the persistent LDS-resident kernel
     BinnedPlan bin{};
+    GenericBig big{};              // PATH_GENERIC receivers above kGenericMaxM entries (round_generic.hip)
+    bool generic_small = true;     // PATH_GENERIC: some receiver has at most kGenericMaxM entries
     MsgParams mp{};
     double* x[2] = {nullptr, nullptr};   // x[k] = xb(k): the synchronous double buffer
     double* xall = nullptr;        // H value buffers of B*Npad (+2) doubles, x^q in buffer q % H
@@ -236,6 +238,7 @@ static void release(acs_sim* s) {
     (void)hipFree(s->xall);
     (void)hipFree(s->ell);
     binned_free(s->bin);
+    generic_big_free(s->big);
     (void)hipFree(s->status);
     (void)hipFree(s->st);
     (void)hipFree(s->partial);
@@ -514,7 +517,8 @@ static int enqueue_round(acs_sim* s, uint32_t r) {
             d.bconst = s->mp.bconst;
             HIP_TRY(launch_round_dense(d, s->stream));
         } else {
-            HIP_TRY(launch_round_generic(a, s->B, s->stream));
+            if (s->generic_small) HIP_TRY(launch_round_generic(a, s->B, s->stream));
+            HIP_TRY(launch_round_generic_big(s->big, a, s->B, s->stream));
         }
         if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
         const FinalizeArgs fin = make_finalize(s, r + 1, s->partial, s->nblk, false);
@@ -821,14 +825,16 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         s->csr_var = true;
         s->dp = s->d;
         s->kname = std::string("k_round_regular<") + std::to_string(s->d) + "," + std::to_string(cfg->trim) + ",csr>";
-    } else if (s->m <= kGenericMaxM) {
+    } else if (s->m <= kGenericBigMaxM) {
         s->path = PATH_GENERIC;
-        s->kname = "k_round_generic";
+        s->generic_small = !(cfg->topology == ACS_TOPO_COMPLETE && s->m > kGenericMaxM);
+        s->kname = s->m <= kGenericMaxM ? "k_round_generic"
+                   : s->generic_small   ? "k_round_generic+k_big_resolve+sort+k_big_rule"
+                                        : "k_big_resolve+sort+k_big_rule";
     } else {
         delete s;
-        return fail(ACS_EUNSUPPORTED, "m = %llu entries per receiver exceeds the generic kernel's %u",
-                    (unsigned long long)(cfg->topology == ACS_TOPO_COMPLETE ? cfg->n_nodes : cfg->degree + 1ull),
-                    kGenericMaxM);
+        return fail(ACS_EUNSUPPORTED, "m = %llu entries per receiver exceeds the big-m generic path's %llu",
+                    (unsigned long long)s->m, (unsigned long long)kGenericBigMaxM);
     }
     if (cfg->fault_model != ACS_FAULT_NONE && s->N >= (1ull << 31)) {   // (any B: setup.hip batches instances)
         delete s;
@@ -971,6 +977,18 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
                 s->ell = nullptr;
             }
         }
+    }
+    if (s->path == PATH_GENERIC && s->m > kGenericMaxM) {   // receivers for the big-m path
+        std::vector<uint32_t> ids;
+        std::vector<uint64_t> mv;
+        for (uint64_t i = 0; i < s->N; ++i) {
+            const uint64_t mi = cfg->topology == ACS_TOPO_CSR ? h_rowptr[i + 1] - h_rowptr[i] + 1 : s->m;
+            if (mi > kGenericMaxM) {
+                ids.push_back((uint32_t)i);
+                mv.push_back(mi);
+            }
+        }
+        CREATE_TRY(generic_big_build(s->big, ids, mv, s->f32, s->stream));
     }
     CREATE_TRY(launch_init_values(s->x[0], s->B, s->N, s->mp.key, cfg->instance_offset, s->f32, s->stream));
     for (Part& q : s->parts)
@@ -1228,7 +1246,7 @@ int acs_get_spread_trace(acs_sim* s, uint64_t b, double* out, uint64_t n, uint64
 int acs_set_state(acs_sim* s, uint32_t round, const void* x, uint64_t n) {
     if (!s || !x || n != s->B * s->N) return fail(ACS_EINVAL, "set_state needs B*N values");
     if (round > s->c.max_rounds) return fail(ACS_EINVAL, "round > max_rounds");
-    // Values must be finite and bounded (sums of up to kGenericMaxM of them stay finite, so no
+    // Values must be finite and bounded (sums of up to kGenericBigMaxM = 2^27 of them stay finite, so no
     // NaN can ever appear in x: the tagged binned phase B reads every quiet NaN as a sender tag),
     // and -0.0 is canonicalised to +0.0 (sorted value sequences stay unique).
     std::vector<unsigned char> canon(n * s->es);

@@ -13,6 +13,8 @@
 //   trace     : f64 [B][max_rounds+1] optional spread trace
 #pragma once
 
+#include <utility>
+#include <vector>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -178,8 +180,30 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
                                const FinalizeArgs* fin = nullptr, uint32_t phases = 7, SrcSel sel = SrcSel{});
 
 // Generic kernel: one workgroup per receiver, LDS bitonic sort (any topology, m <= 8192).
-constexpr uint32_t kGenericMaxM = 8192;
+constexpr uint32_t kGenericMaxM = 8192;   // receivers with more entries take the big-m path
 hipError_t launch_round_generic(const RoundArgs& a, uint64_t B, hipStream_t s);
+// big-m path (round_generic.hip): receivers with kGenericMaxM < m_i <= kGenericBigMaxM, entries
+// in global scratch (batches of at most kGenericBigCap entries), segmented radix sort, rule.
+// kGenericBigMaxM keeps every sum of admitted values (|x| <= 1e300) finite.
+constexpr uint64_t kGenericBigMaxM = 1ull << 27;
+constexpr uint64_t kGenericBigCap = 1ull << 27;
+struct GenericBig {
+    uint64_t n = 0, cap = 0;                 // receivers on the path, scratch entries per batch
+    bool f32 = false;
+    uint32_t* ids = nullptr;                 // [n] receiver ids
+    uint64_t* eoff = nullptr;                // [n+1] segment offsets (device)
+    std::vector<uint64_t> h_eoff;            // the same on the host (batch bases)
+    std::vector<std::pair<uint64_t, uint64_t>> batches;   // [k0, k1) ranges of ids
+    void* ent = nullptr;                     // [cap] resolved entries (then tree-sum scratch)
+    void* srt = nullptr;                     // [cap] sorted entries
+    uint32_t* nmiss = nullptr;               // [max batch] entries left out (OMIT)
+    void* temp = nullptr;                    // hipCUB scratch
+    size_t temp_bytes = 0;
+};
+hipError_t generic_big_build(GenericBig& g, const std::vector<uint32_t>& ids, const std::vector<uint64_t>& m_of,
+                             bool f32, hipStream_t s);
+void generic_big_free(GenericBig& g);
+hipError_t launch_round_generic_big(const GenericBig& g, const RoundArgs& a, uint64_t B, hipStream_t s);
 
 // Dense shared-sort kernels (round_dense.hip): COMPLETE topology, no loss, sort-based rule,
 // no crash faults, Byzantine SPLIT/CONSTANT; one instance.

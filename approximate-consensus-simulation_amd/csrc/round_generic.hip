@@ -1,10 +1,13 @@
 // round_generic.hip — general-purpose round kernel: one 256-thread workgroup per receiver.
 //
 // Covers every (topology, m <= 8192, rule, t, fault, loss) combination the register kernels do
-// not: the workgroup resolves the m entries (§A.6) into LDS, bitonic-sorts them in LDS padded to
+// not (receivers with more entries take the big-m path at the end of this file): the workgroup resolves the m entries (§A.6) into LDS, bitonic-sorts them in LDS padded to
 // a power of two with +inf (§A.7; a sort network, so the sorted sequence — and therefore the
 // tree sum — is the spec's), then applies the rule with an LDS stride-halving tree sum.
 // Used for the dense cfg2 shape (N = 1024 complete, t = 341) and any odd (d, t).
+#include <hipcub/hipcub.hpp>
+
+#include <cstdlib>
 #include <mutex>
 
 #include "resolve.hpp"
@@ -42,6 +45,46 @@ __device__ __forceinline__ void block_bitonic_sort(VT* v, uint32_t P) {
     }
 }
 
+// Entry e of receiver i (§A.3 topology order, §A.5 drop, §A.4 / §A.6 resolution, bounded delay):
+// the value that goes into S_i, or omit_fill with out = true when missing_policy = OMIT leaves it out.
+template <typename VT>
+__device__ __forceinline__ VT generic_entry(const RoundArgs& a, uint32_t lb, uint32_t b, uint32_t bG, uint32_t i,
+                                            uint64_t rp, uint32_t e, const VT* __restrict__ x,
+                                            const uint32_t* __restrict__ stv, VT xi, VT lo, VT hi, bool& out) {
+    const MsgParams& mp = a.mp;
+    const uint64_t N = a.N;
+    const uint32_t r = a.r;
+    out = false;
+    uint32_t j;
+    uint64_t slot;
+    bool self;
+    if (a.topology == 0) {   // COMPLETE: entry j from node j, slot i*N + j
+        j = e;
+        slot = (uint64_t)i * N + j;
+        self = j == i;
+    } else if (a.topology == 2) {   // CSR: entry 0 self, entry 1+t from colidx[rp+t]
+        self = e == 0;
+        j = self ? i : a.colidx[rp + e - 1];
+        slot = rp + e - 1;
+    } else {                 // RANDOM_REGULAR: entry 0 self, entry 1+t from nbr(i,t)
+        self = e == 0;
+        const uint32_t t = e - 1;
+        j = self ? i : a.ell[(((uint64_t)(i >> 6) * (a.dp >> 2) + (t >> 2)) * 64 + (i & 63)) * 4 + (t & 3)];
+        slot = (uint64_t)i * a.d + t;
+    }
+    if (self) return xi;
+    const uint32_t stj = stv ? stv[j] : kHonest;
+    const bool dropped = mp.thr && draw(mp.key, kStreamDrop, bG, r, slot) < mp.thr;
+    const VT xj = a.delay ? delayed_x<VT>(a, lb, r, draw(mp.key, kStreamDelay, b, r, slot), j) : x[j];
+    bool miss;
+    const VT v = resolve_entry_m(mp, stj, xj, xi, dropped, b, r, i, slot, lo, hi, miss);
+    if (mp.omit && miss) {
+        out = true;
+        return omit_fill<VT>(a.rule);
+    }
+    return v;
+}
+
 // VT = double, or float in fp32 mode
 template <typename VT>
 __global__ __launch_bounds__(kGenericBlock) void k_round_generic(const RoundArgs a, uint32_t P) {
@@ -68,13 +111,13 @@ __global__ __launch_bounds__(kGenericBlock) void k_round_generic(const RoundArgs
     const MsgParams& mp = a.mp;
     const uint32_t b = (uint32_t)(mp.inst_offset + lb);
     const uint32_t bG = b - b % mp.mask_group;
-    const uint32_t r = a.r;
     uint32_t m = a.m;
     uint64_t rp = 0;
     if (a.topology == 2) {   // CSR: m_i = deg(i) + 1 (a.m is the maximum, which sized P)
         rp = a.rowptr[i];
         m = (uint32_t)(a.rowptr[i + 1] - rp) + 1;
     }
+    if (m > P) return;   // above kGenericMaxM: the big-m path (below) handles this receiver
     const VT lo = (VT)S->lo, hi = (VT)S->hi;
     const bool avg = a.rule == 0;
     __shared__ uint32_t nmiss_s;   // entries left out under missing_policy = OMIT
@@ -86,36 +129,9 @@ __global__ __launch_bounds__(kGenericBlock) void k_round_generic(const RoundArgs
         if (e >= m) {
             v = avg ? VT(0) : (VT)kInf;
         } else {
-            uint32_t j;
-            uint64_t slot;
-            bool self;
-            if (a.topology == 0) {   // COMPLETE: entry j from node j, slot i*N + j
-                j = e;
-                slot = (uint64_t)i * N + j;
-                self = j == i;
-            } else if (a.topology == 2) {   // CSR: entry 0 self, entry 1+t from colidx[rp+t]
-                self = e == 0;
-                j = self ? i : a.colidx[rp + e - 1];
-                slot = rp + e - 1;
-            } else {                 // RANDOM_REGULAR: entry 0 self, entry 1+t from nbr(i,t)
-                self = e == 0;
-                const uint32_t t = e - 1;
-                j = self ? i : a.ell[(((uint64_t)(i >> 6) * (a.dp >> 2) + (t >> 2)) * 64 + (i & 63)) * 4 + (t & 3)];
-                slot = (uint64_t)i * a.d + t;
-            }
-            if (self) {
-                v = xi;
-            } else {
-                const uint32_t stj = stv ? stv[j] : kHonest;
-                const bool dropped = mp.thr && draw(mp.key, kStreamDrop, bG, r, slot) < mp.thr;
-                const VT xj = a.delay ? delayed_x<VT>(a, lb, r, draw(mp.key, kStreamDelay, b, r, slot), j) : x[j];
-                bool miss;
-                v = resolve_entry_m(mp, stj, xj, xi, dropped, b, r, i, slot, lo, hi, miss);
-                if (mp.omit && miss) {
-                    v = omit_fill<VT>(a.rule);
-                    ++nmiss;
-                }
-            }
+            bool out;
+            v = generic_entry<VT>(a, lb, b, bG, i, rp, e, x, stv, xi, lo, hi, out);
+            nmiss += out;
         }
         sh[e] = v;
     }
@@ -167,10 +183,249 @@ __global__ __launch_bounds__(kGenericBlock) void k_round_generic(const RoundArgs
     }
 }
 
+
+// ------------------------------------------------------------------------------ big m
+// Receivers with m_i > kGenericMaxM (complete graphs above 8192 nodes, CSR hubs; m_i <=
+// kGenericBigMaxM): the entries go to global scratch, a hipCUB segmented radix sort orders each
+// receiver's segment (sort-based rules), and one workgroup per receiver applies the rule with the
+// same stride-halving sums in global memory.  Receivers are processed in batches of at most
+// GenericBig::cap entries; g.ids lists them, g.eoff[k] is the scratch offset of ids[k]'s segment.
+template <typename VT>
+__device__ __forceinline__ VT big_inst_ptrs(const RoundArgs& a, uint32_t lb, uint32_t i, const VT*& x, VT*& xo,
+                                            const uint32_t*& stv, uint32_t& si) {
+    x = reinterpret_cast<const VT*>(a.xin) + (uint64_t)lb * a.N;
+    xo = reinterpret_cast<VT*>(a.xout) + (uint64_t)lb * a.N;
+    stv = a.status ? a.status + (uint64_t)lb * a.N : nullptr;
+    si = stv ? stv[i] : kHonest;
+    return x[i];
+}
+
+template <typename VT>
+__global__ __launch_bounds__(kGenericBlock) void k_big_resolve(const RoundArgs a, uint32_t lb,
+                                                               const uint32_t* __restrict__ ids,
+                                                               const uint64_t* __restrict__ eoff, uint64_t k0,
+                                                               VT* __restrict__ ent, uint32_t* __restrict__ nmiss_out) {
+    const InstState* S = a.st + lb;
+    if (S->done) return;
+    const uint64_t k = k0 + blockIdx.x;
+    const uint32_t i = ids[k];
+    const uint64_t o = eoff[k] - eoff[k0];
+    const uint32_t m = (uint32_t)(eoff[k + 1] - eoff[k]);
+    const VT* x;
+    VT* xo;
+    const uint32_t* stv;
+    uint32_t si;
+    const VT xi = big_inst_ptrs<VT>(a, lb, i, x, xo, stv, si);
+    if (!is_active(si, a.r)) return;   // frozen value; the rule kernel writes it
+    const uint32_t b = (uint32_t)(a.mp.inst_offset + lb);
+    const uint32_t bG = b - b % a.mp.mask_group;
+    const uint64_t rp = a.topology == 2 ? a.rowptr[i] : 0;
+    const VT lo = (VT)S->lo, hi = (VT)S->hi;
+    uint32_t nmiss = 0;
+    for (uint32_t e = threadIdx.x; e < m; e += kGenericBlock) {
+        bool out;
+        ent[o + e] = generic_entry<VT>(a, lb, b, bG, i, rp, e, x, stv, xi, lo, hi, out);
+        nmiss += out;
+    }
+    __shared__ uint32_t nm_s;
+    if (threadIdx.x == 0) nm_s = 0;
+    __syncthreads();
+    if (nmiss) atomicAdd(&nm_s, nmiss);
+    __syncthreads();
+    if (threadIdx.x == 0) nmiss_out[blockIdx.x] = nm_s;
+}
+
+// §A.7 tree_sum of v(q) = q < cnt ? src[off + q*step] : 0 over q < P2 (the next power of two), in
+// w (which may alias src when off = 0 and step = 1): the first pass reads src, later passes run in
+// place; every pass is the stride-halving pass of the LDS kernels.
+template <typename VT>
+__device__ VT big_tree_sum(const VT* src, VT* w, uint64_t off, uint64_t step, uint64_t cnt) {
+    uint64_t P2 = 1;
+    while (P2 < cnt) P2 <<= 1;
+    if (P2 == 1) return src[off];
+    uint64_t s = P2 >> 1;
+    for (uint64_t k = threadIdx.x; k < s; k += kGenericBlock) {
+        const VT u = src[off + k * step];
+        const VT v = k + s < cnt ? src[off + (k + s) * step] : VT(0);
+        w[k] = u + v;
+    }
+    __syncthreads();
+    for (s >>= 1; s >= 1; s >>= 1) {
+        for (uint64_t k = threadIdx.x; k < s; k += kGenericBlock) w[k] = w[k] + w[k + s];
+        __syncthreads();
+    }
+    return w[0];
+}
+
+template <typename VT>
+__global__ __launch_bounds__(kGenericBlock) void k_big_rule(const RoundArgs a, uint32_t lb, const uint32_t* __restrict__ ids,
+                                                            const uint64_t* __restrict__ eoff, uint64_t k0,
+                                                            const VT* srt, VT* wsp, const uint32_t* __restrict__ nmiss_in) {
+    const InstState* S = a.st + lb;
+    if (S->done) return;
+    const uint64_t k = k0 + blockIdx.x;
+    const uint32_t i = ids[k];
+    const uint64_t o = eoff[k] - eoff[k0];
+    const VT* x;
+    VT* xo;
+    const uint32_t* stv;
+    uint32_t si;
+    const VT xi = big_inst_ptrs<VT>(a, lb, i, x, xo, stv, si);
+    double2* part = a.partial + (uint64_t)lb * a.nblk + i;
+    if (!is_active(si, a.r)) {   // Byzantine or crashed: value frozen (§A.6); never honest
+        if (threadIdx.x == 0) {
+            xo[i] = xi;
+            *part = make_double2(kInf, -kInf);
+        }
+        return;
+    }
+    const uint32_t m = (uint32_t)(eoff[k + 1] - eoff[k]) - nmiss_in[blockIdx.x];   // m' (OMIT)
+    const VT* v = srt + o;
+    VT* w = wsp + o;
+    const uint32_t t = a.trim;
+    VT res;
+    if (a.rule == 0) {
+        res = big_tree_sum<VT>(v, w, 0, 1, (uint64_t)(eoff[k + 1] - eoff[k])) / (VT)m;   // fillers add +0.0
+    } else if (a.rule != 4 && m <= 2 * t) {   // OMIT: too few entries to trim, keep x_i
+        res = xi;
+    } else if (a.rule == 4) {   // W-MSR
+        uint32_t lo_ = 0, hi_ = m;
+        while (lo_ < hi_) { const uint32_t md = (lo_ + hi_) >> 1; if (v[md] < xi) lo_ = md + 1; else hi_ = md; }
+        const uint32_t nl = lo_;
+        hi_ = m;
+        while (lo_ < hi_) { const uint32_t md = (lo_ + hi_) >> 1; if (v[md] <= xi) lo_ = md + 1; else hi_ = md; }
+        const uint32_t ng = m - lo_;
+        const uint32_t wlo = nl < t ? nl : t, whi = ng < t ? ng : t, cnt = m - wlo - whi;
+        res = big_tree_sum<VT>(v, w, wlo, 1, cnt) / (VT)cnt;
+    } else if (a.rule == 2) {
+        res = (v[t] + v[m - t - 1]) * VT(0.5);
+    } else {
+        const uint32_t nr = m - 2 * t;
+        const uint32_t step = a.rule == 3 ? t : 1;
+        const uint32_t cnt = a.rule == 3 ? (nr + t - 1) / t : nr;
+        res = big_tree_sum<VT>(v, w, t, step, cnt) / (VT)cnt;
+    }
+    if (threadIdx.x == 0) {
+        xo[i] = res;
+        *part = si == kHonest ? make_double2((double)res, (double)res) : make_double2(kInf, -kInf);
+    }
+}
+
+namespace {
+struct SubBase {
+    uint64_t base;
+    __host__ __device__ uint64_t operator()(uint64_t v) const { return v - base; }
+};
+using BigOffIt = hipcub::TransformInputIterator<uint64_t, SubBase, const uint64_t*>;
+
+template <typename VT>
+hipError_t big_sort(void* temp, size_t& bytes, const VT* in, VT* out, uint64_t n, uint64_t nseg, const uint64_t* eoff_k0,
+                    uint64_t base, hipStream_t s) {
+    const BigOffIt beg(eoff_k0, SubBase{base});
+    return hipcub::DeviceSegmentedRadixSort::SortKeys(temp, bytes, in, out, (int)n, (int)nseg, beg, beg + 1, 0,
+                                                      (int)(sizeof(VT) * 8), s);
+}
+}  // namespace
+
+hipError_t generic_big_build(GenericBig& g, const std::vector<uint32_t>& ids, const std::vector<uint64_t>& m_of,
+                             bool f32, hipStream_t s) {
+    g = GenericBig{};
+    if (ids.empty()) return hipSuccess;
+    const uint64_t es = f32 ? 4 : 8;
+    g.h_eoff.resize(ids.size() + 1);
+    g.h_eoff[0] = 0;
+    uint64_t mx = 0;
+    for (size_t k = 0; k < ids.size(); ++k) {
+        g.h_eoff[k + 1] = g.h_eoff[k] + m_of[k];
+        mx = m_of[k] > mx ? m_of[k] : mx;
+    }
+    if (mx > kGenericBigMaxM) return hipErrorNotSupported;
+    g.cap = g.h_eoff.back() < kGenericBigCap ? g.h_eoff.back() : kGenericBigCap;
+    if (g.cap < mx) g.cap = mx;
+    if (const char* v = getenv("ACSIM_BIG_CAP")) {   // tests: several batches on small configs
+        const uint64_t c = strtoull(v, nullptr, 10);
+        if (c >= mx && c < g.cap) g.cap = c;
+    }
+    // batches: consecutive receivers whose segments fit cap
+    uint64_t maxseg = 0;
+    for (uint64_t k0 = 0; k0 < ids.size();) {
+        uint64_t k1 = k0 + 1;
+        while (k1 < ids.size() && g.h_eoff[k1 + 1] - g.h_eoff[k0] <= g.cap) ++k1;
+        g.batches.push_back({k0, k1});
+        maxseg = k1 - k0 > maxseg ? k1 - k0 : maxseg;
+        k0 = k1;
+    }
+    g.f32 = f32;
+    g.n = ids.size();
+    hipError_t e = hipMalloc(&g.ids, ids.size() * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&g.eoff, g.h_eoff.size() * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc(&g.ent, g.cap * es);
+    if (e == hipSuccess) e = hipMalloc(&g.srt, g.cap * es);
+    if (e == hipSuccess) e = hipMalloc(&g.nmiss, maxseg * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemcpy(g.ids, ids.data(), ids.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(g.eoff, g.h_eoff.data(), g.h_eoff.size() * sizeof(uint64_t), hipMemcpyHostToDevice);
+    // sort scratch: the largest requirement over the batches
+    for (const auto& bt : g.batches) {
+        if (e != hipSuccess) break;
+        size_t bytes = 0;
+        const uint64_t n = g.h_eoff[bt.second] - g.h_eoff[bt.first];
+        e = f32 ? big_sort<float>(nullptr, bytes, nullptr, nullptr, n, bt.second - bt.first, g.eoff + bt.first,
+                                  g.h_eoff[bt.first], s)
+                : big_sort<double>(nullptr, bytes, nullptr, nullptr, n, bt.second - bt.first, g.eoff + bt.first,
+                                   g.h_eoff[bt.first], s);
+        g.temp_bytes = bytes > g.temp_bytes ? bytes : g.temp_bytes;
+    }
+    if (e == hipSuccess) e = hipMalloc(&g.temp, g.temp_bytes ? g.temp_bytes : 16);
+    if (e != hipSuccess) generic_big_free(g);
+    return e;
+}
+
+void generic_big_free(GenericBig& g) {
+    (void)hipFree(g.ids);
+    (void)hipFree(g.eoff);
+    (void)hipFree(g.ent);
+    (void)hipFree(g.srt);
+    (void)hipFree(g.nmiss);
+    (void)hipFree(g.temp);
+    g = GenericBig{};
+}
+
+template <typename VT>
+static hipError_t big_round(const GenericBig& g, const RoundArgs& a, uint64_t B, hipStream_t s) {
+    VT* ent = reinterpret_cast<VT*>(g.ent);
+    VT* srt = reinterpret_cast<VT*>(g.srt);
+    const bool sorted = a.rule != 0;
+    for (uint64_t lb = 0; lb < B; ++lb) {
+        for (const auto& bt : g.batches) {
+            const uint64_t k0 = bt.first, nk = bt.second - bt.first;
+            hipLaunchKernelGGL(k_big_resolve<VT>, dim3((unsigned)nk), dim3(kGenericBlock), 0, s, a, (uint32_t)lb, g.ids,
+                               g.eoff, k0, ent, g.nmiss);
+            if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+            if (sorted) {
+                size_t bytes = g.temp_bytes;
+                if (hipError_t e = big_sort<VT>(g.temp, bytes, ent, srt, g.h_eoff[bt.second] - g.h_eoff[k0], nk,
+                                                g.eoff + k0, g.h_eoff[k0], s);
+                    e != hipSuccess)
+                    return e;
+            }
+            hipLaunchKernelGGL(k_big_rule<VT>, dim3((unsigned)nk), dim3(kGenericBlock), 0, s, a, (uint32_t)lb, g.ids,
+                               g.eoff, k0, sorted ? (const VT*)srt : (const VT*)ent, ent, g.nmiss);
+            if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+        }
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_round_generic_big(const GenericBig& g, const RoundArgs& a, uint64_t B, hipStream_t s) {
+    if (!g.n) return hipSuccess;
+    return g.f32 ? big_round<float>(g, a, B, s) : big_round<double>(g, a, B, s);
+}
+
 hipError_t launch_round_generic(const RoundArgs& a, uint64_t B, hipStream_t s) {
+    // receivers above kGenericMaxM entries return at once (the big-m path serves them)
     uint32_t P = 1;
-    while (P < a.m) P <<= 1;
-    if (P > kGenericMaxM) return hipErrorNotSupported;
+    while (P < a.m && P < kGenericMaxM) P <<= 1;
     const size_t lds = 2 * (size_t)P * (a.f32 ? sizeof(float) : sizeof(double));
     {   // > 64 KiB of dynamic LDS: the attribute is per device, set once per device ordinal
         constexpr int kMaxDev = 64;

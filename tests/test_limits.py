@@ -1,9 +1,13 @@
-"""Size limits lifted in round 3: fault schedules of any B·N (the segmented sort
-of the §A.4 fault keys runs in instance batches, setup.hip build_fault_status).
+"""Size limits lifted in round 3.
 
-GPU only: the forced multi-batch schedule against the oracle, and a B·N > 2^31 batch whose
-sampled instances (fault set, crash rounds, x after two rounds) match the oracle run of that
-instance alone (instance_offset = its global id, SURVEY §A.1 counters).
+- Fault schedules of any B·N: the segmented sort of the §A.4 fault keys runs in instance batches
+  (setup.hip build_fault_status).  The forced multi-batch schedule against the oracle, and a
+  B·N > 2^31 batch whose sampled instances (fault set, x after two rounds) match the oracle run of
+  that instance alone (instance_offset = its global id, SURVEY §A.1 counters).
+- Receivers with more than 8192 entries (complete graphs above 8192 nodes, CSR hubs): the big-m
+  generic path (round_generic.hip: global scratch, segmented radix sort, global stride-halving
+  sums), bit-exact against the oracle for every rule, OMIT, fp32, delay and several instances, with
+  forced small batches (ACSIM_BIG_CAP) as well.
 """
 import contextlib
 import os
@@ -75,3 +79,72 @@ def test_fault_schedule_above_2e31(oracle_mod):
             o.run()
             assert np.array_equal(o.fault_status().reshape(-1), got[b][0]), b
             assert np.array_equal(bits(o.values(0)), bits(got[b][1])), b
+
+
+def gpu_vs_oracle(oracle_mod, cfg, csr=None, **envs):
+    with env(**envs), acsim.Simulator(cfg, device=0, csr=csr) as g:
+        kname = g.kernel_name()
+        g.run()
+        r, x = g.rounds(), g.all_values()
+    with oracle_mod.OracleSimulator(cfg, threads=8, csr=csr) as o:
+        o.run()
+        assert np.array_equal(o.rounds(), r)
+        xo = o.all_values()
+    xv = np.ascontiguousarray(x)
+    view = np.uint64 if xv.dtype == np.float64 else np.uint32
+    assert np.array_equal(np.ascontiguousarray(xo).view(view), xv.view(view))
+    return kname
+
+
+BIG = dict(n_nodes=8300, topology="complete", termination="fixed", max_rounds=2, seed=31)
+BIG_CASES = {
+    "avg_loss": dict(rule="average", trim=0, loss_p=0.3),
+    "trimmed_crash_loss": dict(rule="trimmed", trim=100, loss_p=0.3, fault_model="crash", n_faulty=400, crash_window=2),
+    "midpoint_byz_random": dict(rule="midpoint", trim=300, fault_model="byzantine", n_faulty=300,
+                                byz_strategy="random", byz_delta=0.2),
+    "dlpsw_loss": dict(rule="dlpsw", trim=7, loss_p=0.25),
+    "wmsr_crash": dict(rule="wmsr", trim=50, fault_model="crash", n_faulty=200, crash_window=3, loss_p=0.1),
+    "trimmed_omit": dict(rule="trimmed", trim=40, loss_p=0.4, fault_model="crash", n_faulty=300, crash_window=2,
+                         missing_policy="omit"),
+    "avg_omit": dict(rule="average", trim=0, loss_p=0.4, missing_policy="omit"),
+    "f32_trimmed": dict(rule="trimmed", trim=60, loss_p=0.2, dtype="f32"),
+    "delay_trimmed": dict(rule="trimmed", trim=30, loss_p=0.1, delay_max=2, max_rounds=4),
+    "instances_avg": dict(rule="average", trim=0, loss_p=0.3, n_instances=3, instance_offset=2),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(BIG_CASES))
+def test_big_m_complete_matches_oracle(oracle_mod, name):
+    cfg = Config(**{**BIG, **BIG_CASES[name]})
+    kname = gpu_vs_oracle(oracle_mod, cfg)
+    assert kname.startswith("k_big_resolve"), kname
+
+
+@pytest.mark.gpu
+def test_big_m_forced_batches(oracle_mod):
+    cfg = Config(**{**BIG, **BIG_CASES["trimmed_crash_loss"]})
+    gpu_vs_oracle(oracle_mod, cfg, ACSIM_BIG_CAP=3 * 8300 + 17)   # 3 receivers per batch
+
+
+def hub_csr(n, hubs, seed):
+    """A CSR graph whose rows have 6..20 entries, except `hubs` rows of 8500..12000 entries."""
+    rng = np.random.default_rng(seed)
+    deg = rng.integers(6, 21, size=n)
+    hub_rows = rng.choice(n, size=hubs, replace=False)
+    deg[hub_rows] = rng.integers(8500, 12001, size=hubs)
+    rowptr = np.zeros(n + 1, dtype=np.uint64)
+    rowptr[1:] = np.cumsum(deg)
+    colidx = rng.integers(0, n, size=int(rowptr[-1])).astype(np.uint32)
+    return rowptr, colidx
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rule,t", [("trimmed", 2), ("average", 0), ("wmsr", 3), ("midpoint", 2)])
+def test_big_m_csr_hubs_match_oracle(oracle_mod, rule, t):
+    """Hubs on the big-m path beside ordinary rows on the LDS kernel, in one round."""
+    rowptr, colidx = hub_csr(20000, 7, 37)
+    cfg = Config(n_nodes=20000, topology="csr", rule=rule, trim=t, loss_p=0.2, termination="fixed", max_rounds=3,
+                 seed=41)
+    kname = gpu_vs_oracle(oracle_mod, cfg, csr=(rowptr, colidx), ACSIM_CSR_FAST=0)
+    assert "k_big_resolve" in kname and kname.startswith("k_round_generic"), kname
