@@ -112,6 +112,21 @@ struct acs_sim {
     bool csr_var = false;          // CSR on the register / binned paths: padded ELL of a compiled degree
     uint8_t* deg = nullptr;        // [N] deg(i) (csr_var)
     uint8_t* sw = nullptr;         // [ceil(N/64)] SELL-64 slice widths in 4-wide groups (csr_var)
+    // CSR hub rows (deg > d beside a fast path): the generic kernel over hub_ids (rows with at most
+    // kGenericMaxM entries) and the big-m path (the rest); their partial slots follow the fast
+    // path's nblk_fast block partials
+    // CSR rows on the generic kernel go by size class (LDS per workgroup sized to the class):
+    // gen_ids = the listed rows, class k = gen_ids[gcls[k].off, +n) with every m_i <= gcls[k].P;
+    // row gen_ids[q]'s partial slot is gen_base + q
+    struct GenClass {
+        uint64_t off, n;
+        uint32_t P;
+    };
+    uint32_t* gen_ids = nullptr;
+    std::vector<GenClass> gcls;
+    uint32_t gen_base = 0;
+    uint64_t n_hub = 0;
+    uint32_t nblk_fast = 0;
     double* dsorted = nullptr;     // dense path: sorted base multiset [N]
     uint32_t* dcounts = nullptr;   // dense path: |B|, #Byzantine, #crash-silent
     std::vector<Part> parts;       // virtual partitions 1..P-1 (partition 0 uses x / ell)
@@ -247,6 +262,7 @@ static void release(acs_sim* s) {
     (void)hipFree(s->colidx);
     (void)hipFree(s->deg);
     (void)hipFree(s->sw);
+    (void)hipFree(s->gen_ids);
     (void)hipFree(s->dsorted);
     (void)hipFree(s->dcounts);
     (void)hipFree(s->n_done);
@@ -492,7 +508,9 @@ static int enqueue_round(acs_sim* s, uint32_t r) {
     if (rc) return rc;
     if (!s->partitioned) {
         if (s->binned) {
-            HIP_TRY(launch_round_binned(s->bin, a, s->clean, s->stream, s->fin_pending ? &s->fin_args : nullptr));
+            RoundArgs ab = a;
+            if (s->n_hub) ab.qhi = s->nblk_fast;   // the hub rows' partial slots are the generic kernel's
+            HIP_TRY(launch_round_binned(s->bin, ab, s->clean, s->stream, s->fin_pending ? &s->fin_args : nullptr));
             s->fin_pending = false;
         } else if (s->path == PATH_REGULAR) {
             HIP_TRY(launch_round_regular(a, s->B, s->clean, s->stream));
@@ -516,8 +534,19 @@ static int enqueue_round(acs_sim* s, uint32_t r) {
             d.delta = s->mp.delta;
             d.bconst = s->mp.bconst;
             HIP_TRY(launch_round_dense(d, s->stream));
-        } else {
+        } else if (s->c.topology != ACS_TOPO_CSR) {   // complete / regular graphs: one size for all
             if (s->generic_small) HIP_TRY(launch_round_generic(a, s->B, s->stream));
+            HIP_TRY(launch_round_generic_big(s->big, a, s->B, s->stream));
+        }
+        if (s->c.topology == ACS_TOPO_CSR && (s->path == PATH_GENERIC || s->n_hub)) {
+            // CSR rows on the generic kernels (every row, or the hub rows after the fast path):
+            // by size class, then the rows above kGenericMaxM on the big-m path
+            for (const auto& c : s->gcls) {
+                RoundArgs ah = a;
+                ah.rid = s->gen_ids + c.off;
+                ah.pbase = s->gen_base + (uint32_t)c.off;
+                HIP_TRY(launch_round_generic(ah, s->B, s->stream, c.n, c.P));
+            }
             HIP_TRY(launch_round_generic_big(s->big, a, s->B, s->stream));
         }
         if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
@@ -709,6 +738,23 @@ static uint32_t csr_fast_degree(uint64_t maxdeg, uint32_t t, uint32_t rule) {
     return 0;
 }
 
+// CSR graphs whose largest degree is above every compiled degree: the largest compiled degree d
+// (for this t and rule) whose hub rows (deg > d) are at most a quarter of the rows; 0 if none.
+// The hub rows go to the generic kernel, the rest to the register / binned path padded to d.
+static uint32_t csr_hub_degree(const uint64_t* rowptr, uint64_t N, uint32_t t, uint32_t rule, uint64_t* nhub) {
+    for (uint32_t d : {32u, 16u, 8u, 4u}) {
+        if (!regular_fast_supported(d, t, rule)) continue;
+        uint64_t h = 0;
+        for (uint64_t i = 0; i < N; ++i) h += rowptr[i + 1] - rowptr[i] > d;
+        if (h * 4 <= N) {
+            *nhub = h;
+            return d;
+        }
+        return 0;   // smaller compiled degrees would only leave more hubs
+    }
+    return 0;
+}
+
 // Build the adjacency rows of partition p into `ell` (sorted when the config allows it).
 static hipError_t build_rows(acs_sim* s, uint32_t* ell, int p) {
     const uint64_t gseed = s->c.graph_seed ? s->c.graph_seed : s->c.seed;
@@ -819,8 +865,10 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         s->path = PATH_REGULAR;
         s->kname = regular_fast_name(s->d, cfg->trim, s->clean);
     } else if (cfg->topology == ACS_TOPO_CSR && !env_off("ACSIM_CSR_FAST") &&
-               (s->d = csr_fast_degree(csr_mmax - 1, cfg->trim, cfg->rule)) != 0) {
-        // §8(f) row 1: rows padded to the smallest compiled degree >= max deg(i) with the same t
+               ((s->d = csr_fast_degree(csr_mmax - 1, cfg->trim, cfg->rule)) != 0 ||
+                (s->d = csr_hub_degree(h_rowptr, s->N, cfg->trim, cfg->rule, &s->n_hub)) != 0)) {
+        // §8(f) row 1: rows padded to the smallest compiled degree >= max deg(i) with the same t, or
+        // (power-law graphs) to the largest compiled degree with the rows above it as hub rows
         s->path = PATH_REGULAR;
         s->csr_var = true;
         s->dp = s->d;
@@ -874,11 +922,14 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
             s->kname = nm;
         }
     }
+    if (s->n_hub) s->kname += "+k_round_generic(hubs)";
     if (s->f32) s->kname += " [f32]";
     s->nblk = s->path == PATH_REGULAR ? (uint32_t)((rows_local + kRegularBlock - 1) / kRegularBlock)
             : s->path == PATH_GENERIC ? (uint32_t)s->N
             : s->path == PATH_DENSE   ? dense_nblk(s->N)
                                       : 0u;
+    s->nblk_fast = s->nblk;
+    s->nblk += (uint32_t)s->n_hub;   // hub rows: one partial slot each, after the fast path's
     s->nblk_init = (uint32_t)((s->N + 255) / 256);
     if (s->nblk_init > 1024) s->nblk_init = 1024;
     const uint64_t nround = (uint64_t)s->nblk * (virt ? nranks : 1);
@@ -978,7 +1029,38 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
             }
         }
     }
-    if (s->path == PATH_GENERIC && s->m > kGenericMaxM) {   // receivers for the big-m path
+    if (s->n_hub || (s->path == PATH_GENERIC && cfg->topology == ACS_TOPO_CSR)) {
+        // CSR rows for the generic kernels: the hub rows beside a fast path, or every row on the
+        // generic path.  Rows up to kGenericMaxM entries by size class, the rest on the big-m path.
+        constexpr uint32_t kCls[] = {64, 256, 1024, 4096, kGenericMaxM};
+        std::vector<uint32_t> lists[5], big;
+        std::vector<uint64_t> mv;
+        for (uint64_t i = 0; i < s->N; ++i) {
+            const uint64_t mi = h_rowptr[i + 1] - h_rowptr[i] + 1;
+            if (s->n_hub && mi - 1 <= s->d) continue;   // a fast-path row
+            if (mi > kGenericMaxM) {
+                big.push_back((uint32_t)i);
+                mv.push_back(mi);
+                continue;
+            }
+            int k = 0;
+            while (mi > kCls[k]) ++k;
+            lists[k].push_back((uint32_t)i);
+        }
+        std::vector<uint32_t> all;
+        for (int k = 0; k < 5; ++k) {
+            if (lists[k].empty()) continue;
+            s->gcls.push_back({all.size(), lists[k].size(), kCls[k]});
+            all.insert(all.end(), lists[k].begin(), lists[k].end());
+        }
+        s->gen_base = s->n_hub ? s->nblk_fast : 0;
+        if (!all.empty()) {
+            CREATE_TRY(hipMalloc(&s->gen_ids, all.size() * sizeof(uint32_t)));
+            CREATE_TRY(hipMemcpy(s->gen_ids, all.data(), all.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        }
+        CREATE_TRY(generic_big_build(s->big, big, mv, s->f32, s->stream));
+        s->big.pbase = s->gen_base + all.size();
+    } else if (s->path == PATH_GENERIC && s->m > kGenericMaxM) {   // receivers for the big-m path
         std::vector<uint32_t> ids;
         std::vector<uint64_t> mv;
         for (uint64_t i = 0; i < s->N; ++i) {

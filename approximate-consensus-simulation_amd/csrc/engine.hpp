@@ -61,9 +61,15 @@ struct RoundArgs {
     // exchange finished chunks while later ones compute); 0, ~0u = every block
     uint32_t qlo, qhi;
     uint64_t* ts;             // diagnostic per-workgroup timestamps (ACSIM_BIN_TS; nullptr otherwise)
+    // generic kernel over a receiver list (CSR hub rows beside a fast path): receiver rid[blockIdx.x],
+    // block partial slot pbase + blockIdx.x; nullptr: receiver blockIdx.x, slot = receiver
+    const uint32_t* rid;
+    uint32_t pbase;
 };
 
 constexpr uint32_t kEllNone = 0xFFFFFFFFu;   // padding column of a CSR row below the compiled degree
+constexpr uint8_t kDegHub = 0xFF;             // deg[] of a CSR hub row (above the compiled degree): the fast
+                                              // kernels skip it, the generic kernel serves it
 
 struct FinalizeArgs {
     InstState* st;
@@ -181,7 +187,8 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool cle
 
 // Generic kernel: one workgroup per receiver, LDS bitonic sort (any topology, m <= 8192).
 constexpr uint32_t kGenericMaxM = 8192;   // receivers with more entries take the big-m path
-hipError_t launch_round_generic(const RoundArgs& a, uint64_t B, hipStream_t s);
+// nrecv: grid over a.rid's list (0: every receiver); Pcls: the list's size class (0: from a.m)
+hipError_t launch_round_generic(const RoundArgs& a, uint64_t B, hipStream_t s, uint64_t nrecv = 0, uint32_t Pcls = 0);
 // big-m path (round_generic.hip): receivers with kGenericMaxM < m_i <= kGenericBigMaxM, entries
 // in global scratch (batches of at most kGenericBigCap entries), segmented radix sort, rule.
 // kGenericBigMaxM keeps every sum of admitted values (|x| <= 1e300) finite.
@@ -189,6 +196,7 @@ constexpr uint64_t kGenericBigMaxM = 1ull << 27;
 constexpr uint64_t kGenericBigCap = 1ull << 27;
 struct GenericBig {
     uint64_t n = 0, cap = 0;                 // receivers on the path, scratch entries per batch
+    uint64_t pbase = ~0ull;                  // partial slot of ids[k]: pbase + k (~0: the receiver id)
     bool f32 = false;
     uint32_t* ids = nullptr;                 // [n] receiver ids
     uint64_t* eoff = nullptr;                // [n+1] segment offsets (device)

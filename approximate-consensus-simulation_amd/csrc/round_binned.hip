@@ -351,7 +351,10 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t li = (uint64_t)b * kBinSB + threadIdx.x;   // local row
     const uint64_t i = a.row0 + li;                              // global receiver
-    const bool live = li < a.nrows;
+    bool live = li < a.nrows;
+    if constexpr (VAR) {   // CSR hub rows (no deliveries in the plan): the generic kernel serves them
+        if (live && a.deg[i] == kDegHub) live = false;
+    }
     const uint2* tb = tiles + (uint64_t)b * (nrun + 1);
     // NP-pass blocks of at most 64 runs: every wave fetches all descriptors first (one per lane)
     // and issues part 0's DMA before anything else is in flight, so the only wait ahead of the

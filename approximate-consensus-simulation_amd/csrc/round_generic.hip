@@ -16,20 +16,20 @@ namespace acs {
 
 constexpr int kGenericBlock = 256;
 
-template <typename VT>
+template <int BLK, typename VT>
 __device__ __forceinline__ VT block_tree_sum(VT* w, uint32_t P) {
     for (uint32_t s = P >> 1; s >= 1; s >>= 1) {
-        for (uint32_t k = threadIdx.x; k < s; k += kGenericBlock) w[k] = w[k] + w[k + s];
+        for (uint32_t k = threadIdx.x; k < s; k += BLK) w[k] = w[k] + w[k + s];
         __syncthreads();
     }
     return w[0];
 }
 
-template <typename VT>
+template <int BLK, typename VT>
 __device__ __forceinline__ void block_bitonic_sort(VT* v, uint32_t P) {
     for (uint32_t k = 2; k <= P; k <<= 1) {
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t idx = threadIdx.x; idx < P; idx += kGenericBlock) {
+            for (uint32_t idx = threadIdx.x; idx < P; idx += BLK) {
                 const uint32_t ixj = idx ^ j;
                 if (ixj > idx) {
                     const VT p = v[idx], q = v[ixj];
@@ -86,11 +86,13 @@ __device__ __forceinline__ VT generic_entry(const RoundArgs& a, uint32_t lb, uin
 }
 
 // VT = double, or float in fp32 mode
-template <typename VT>
-__global__ __launch_bounds__(kGenericBlock) void k_round_generic(const RoundArgs a, uint32_t P) {
+// BLK threads per workgroup: 64 for receivers of at most 64 entries (one wave), 1024 from 2048
+// entries (the serial sort passes of one receiver are the kernel's tail), 256 otherwise.
+template <int BLK, typename VT>
+__global__ __launch_bounds__(BLK) void k_round_generic(const RoundArgs a, uint32_t Pmax) {
     extern __shared__ __attribute__((aligned(16))) unsigned char sh_raw[];
-    VT* sh = reinterpret_cast<VT*>(sh_raw);   // [P] entries + [P] scratch
-    const uint32_t lb = blockIdx.y, i = blockIdx.x;
+    VT* sh = reinterpret_cast<VT*>(sh_raw);   // [Pmax] entries + [Pmax] scratch
+    const uint32_t lb = blockIdx.y, i = a.rid ? a.rid[blockIdx.x] : blockIdx.x;
     InstState* S = a.st + lb;
     if (S->done) return;
     const uint64_t N = a.N;
@@ -100,7 +102,7 @@ __global__ __launch_bounds__(kGenericBlock) void k_round_generic(const RoundArgs
     const VT xi = x[i];
     const uint32_t si = stv ? stv[i] : kHonest;
     const bool honest = si == kHonest;
-    double2* part = a.partial + (uint64_t)lb * a.nblk + i;
+    double2* part = a.partial + (uint64_t)lb * a.nblk + (a.rid ? a.pbase + blockIdx.x : i);
     if (!is_active(si, a.r)) {   // Byzantine or crashed: value frozen (§A.6); never honest
         if (threadIdx.x == 0) {
             xo[i] = xi;
@@ -117,14 +119,18 @@ __global__ __launch_bounds__(kGenericBlock) void k_round_generic(const RoundArgs
         rp = a.rowptr[i];
         m = (uint32_t)(a.rowptr[i + 1] - rp) + 1;
     }
-    if (m > P) return;   // above kGenericMaxM: the big-m path (below) handles this receiver
+    if (m > Pmax) return;   // above kGenericMaxM: the big-m path (below) handles this receiver
+    // this receiver's power of two (CSR rows differ; the sort is a sort and the +0.0 / +inf padding
+    // leaves the tree sum unchanged, so any P >= m gives the spec's result)
+    uint32_t P = 1;
+    while (P < m) P <<= 1;
     const VT lo = (VT)S->lo, hi = (VT)S->hi;
     const bool avg = a.rule == 0;
     __shared__ uint32_t nmiss_s;   // entries left out under missing_policy = OMIT
     if (threadIdx.x == 0) nmiss_s = 0;
     __syncthreads();
     uint32_t nmiss = 0;
-    for (uint32_t e = threadIdx.x; e < P; e += kGenericBlock) {
+    for (uint32_t e = threadIdx.x; e < P; e += BLK) {
         VT v;
         if (e >= m) {
             v = avg ? VT(0) : (VT)kInf;
@@ -140,11 +146,11 @@ __global__ __launch_bounds__(kGenericBlock) void k_round_generic(const RoundArgs
     m -= nmiss_s;   // m' = present entries (OMIT); the fillers sort past them (+inf) or add +0.0
     VT res;
     if (avg) {
-        res = block_tree_sum(sh, P) / (VT)m;
+        res = block_tree_sum<BLK>(sh, P) / (VT)m;
     } else if (a.rule != 4 && m <= 2 * a.trim) {   // OMIT: too few entries to trim, keep x_i
         res = xi;
     } else {
-        block_bitonic_sort(sh, P);
+        block_bitonic_sort<BLK>(sh, P);
         const uint32_t t = a.trim, nr = m - 2 * t;
         if (a.rule == 4) {   // W-MSR: window [min(t, #below), m - min(t, #above))
             uint32_t nl = 0, nle = 0;   // #entries < xi, #entries <= xi (sh is sorted)
@@ -161,9 +167,9 @@ __global__ __launch_bounds__(kGenericBlock) void k_round_generic(const RoundArgs
             uint32_t P2 = 1;
             while (P2 < cnt) P2 <<= 1;
             VT* w = sh + P;
-            for (uint32_t k = threadIdx.x; k < P2; k += kGenericBlock) w[k] = k < cnt ? sh[wlo + k] : VT(0);
+            for (uint32_t k = threadIdx.x; k < P2; k += BLK) w[k] = k < cnt ? sh[wlo + k] : VT(0);
             __syncthreads();
-            res = block_tree_sum(w, P2) / (VT)cnt;
+            res = block_tree_sum<BLK>(w, P2) / (VT)cnt;
         } else if (a.rule == 2) {
             res = (sh[t] + sh[m - t - 1]) * VT(0.5);
         } else {
@@ -172,9 +178,9 @@ __global__ __launch_bounds__(kGenericBlock) void k_round_generic(const RoundArgs
             uint32_t P2 = 1;
             while (P2 < cnt) P2 <<= 1;
             VT* w = sh + P;
-            for (uint32_t k = threadIdx.x; k < P2; k += kGenericBlock) w[k] = k < cnt ? sh[t + k * step] : VT(0);
+            for (uint32_t k = threadIdx.x; k < P2; k += BLK) w[k] = k < cnt ? sh[t + k * step] : VT(0);
             __syncthreads();
-            res = block_tree_sum(w, P2) / (VT)cnt;
+            res = block_tree_sum<BLK>(w, P2) / (VT)cnt;
         }
     }
     if (threadIdx.x == 0) {
@@ -260,7 +266,8 @@ __device__ VT big_tree_sum(const VT* src, VT* w, uint64_t off, uint64_t step, ui
 template <typename VT>
 __global__ __launch_bounds__(kGenericBlock) void k_big_rule(const RoundArgs a, uint32_t lb, const uint32_t* __restrict__ ids,
                                                             const uint64_t* __restrict__ eoff, uint64_t k0,
-                                                            const VT* srt, VT* wsp, const uint32_t* __restrict__ nmiss_in) {
+                                                            const VT* srt, VT* wsp, const uint32_t* __restrict__ nmiss_in,
+                                                            uint64_t pbase) {
     const InstState* S = a.st + lb;
     if (S->done) return;
     const uint64_t k = k0 + blockIdx.x;
@@ -271,7 +278,7 @@ __global__ __launch_bounds__(kGenericBlock) void k_big_rule(const RoundArgs a, u
     const uint32_t* stv;
     uint32_t si;
     const VT xi = big_inst_ptrs<VT>(a, lb, i, x, xo, stv, si);
-    double2* part = a.partial + (uint64_t)lb * a.nblk + i;
+    double2* part = a.partial + (uint64_t)lb * a.nblk + (pbase == ~0ull ? (uint64_t)i : pbase + k);
     if (!is_active(si, a.r)) {   // Byzantine or crashed: value frozen (§A.6); never honest
         if (threadIdx.x == 0) {
             xo[i] = xi;
@@ -410,7 +417,7 @@ static hipError_t big_round(const GenericBig& g, const RoundArgs& a, uint64_t B,
                     return e;
             }
             hipLaunchKernelGGL(k_big_rule<VT>, dim3((unsigned)nk), dim3(kGenericBlock), 0, s, a, (uint32_t)lb, g.ids,
-                               g.eoff, k0, sorted ? (const VT*)srt : (const VT*)ent, ent, g.nmiss);
+                               g.eoff, k0, sorted ? (const VT*)srt : (const VT*)ent, ent, g.nmiss, g.pbase);
             if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
         }
     }
@@ -422,10 +429,12 @@ hipError_t launch_round_generic_big(const GenericBig& g, const RoundArgs& a, uin
     return g.f32 ? big_round<float>(g, a, B, s) : big_round<double>(g, a, B, s);
 }
 
-hipError_t launch_round_generic(const RoundArgs& a, uint64_t B, hipStream_t s) {
-    // receivers above kGenericMaxM entries return at once (the big-m path serves them)
+hipError_t launch_round_generic(const RoundArgs& a, uint64_t B, hipStream_t s, uint64_t nrecv, uint32_t Pcls) {
+    // receivers above kGenericMaxM entries return at once (the big-m path serves them); Pcls: the
+    // size class of a receiver list (every m_i <= Pcls; smaller LDS, more workgroups per CU)
     uint32_t P = 1;
     while (P < a.m && P < kGenericMaxM) P <<= 1;
+    if (Pcls && Pcls < P) P = Pcls;
     const size_t lds = 2 * (size_t)P * (a.f32 ? sizeof(float) : sizeof(double));
     {   // > 64 KiB of dynamic LDS: the attribute is per device, set once per device ordinal
         constexpr int kMaxDev = 64;
@@ -435,17 +444,32 @@ hipError_t launch_round_generic(const RoundArgs& a, uint64_t B, hipStream_t s) {
         if (hipError_t e = hipGetDevice(&dev); e != hipSuccess) return e;
         if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
         std::call_once(once[dev], [dev] {
-            status[dev] = hipFuncSetAttribute((const void*)k_round_generic<double>,
-                                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                                              (int)(2 * kGenericMaxM * sizeof(double)));
+            const int bytes = (int)(2 * kGenericMaxM * sizeof(double));
+            hipError_t e = hipFuncSetAttribute((const void*)k_round_generic<256, double>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void*)k_round_generic<1024, double>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+            status[dev] = e;
         });
         if (status[dev] != hipSuccess) return status[dev];
     }
-    const dim3 grid((unsigned)a.N, (unsigned)B);
-    if (a.f32)
-        hipLaunchKernelGGL(k_round_generic<float>, grid, dim3(kGenericBlock), lds, s, a, P);
+    const dim3 grid((unsigned)(nrecv ? nrecv : a.N), (unsigned)B);
+    const int blk = P <= 64 ? 64 : P >= 2048 ? 1024 : 256;
+#define ACS_GEN_LAUNCH(BB)                                                                                         \
+    {                                                                                                              \
+        if (a.f32)                                                                                                 \
+            hipLaunchKernelGGL((k_round_generic<BB, float>), grid, dim3(BB), lds, s, a, P);                        \
+        else                                                                                                       \
+            hipLaunchKernelGGL((k_round_generic<BB, double>), grid, dim3(BB), lds, s, a, P);                       \
+    }
+    if (blk == 64)
+        ACS_GEN_LAUNCH(64)
+    else if (blk == 1024)
+        ACS_GEN_LAUNCH(1024)
     else
-        hipLaunchKernelGGL(k_round_generic<double>, grid, dim3(kGenericBlock), lds, s, a, P);
+        ACS_GEN_LAUNCH(256)
+#undef ACS_GEN_LAUNCH
     return hipGetLastError();
 }
 

@@ -37,7 +37,7 @@ __global__ __launch_bounds__(kRegularBlock) void k_round_regular(const RoundArgs
     const uint32_t i = (uint32_t)a.row0 + li;                        // global receiver id
 
     double mn = kInf, mx = -kInf;   // exact for binary32 values too
-    if (li < a.nrows && i < N) {
+    if (li < a.nrows && i < N && !(VAR && a.deg[i] == kDegHub)) {   // (CSR hub rows: the generic kernel)
         const VT xi = x[i];
         VT res = xi;
         bool honest = true, active = true;

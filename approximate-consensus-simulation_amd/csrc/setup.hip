@@ -84,8 +84,10 @@ __global__ __launch_bounds__(256) void k_csr_to_ell(const uint64_t* __restrict__
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= N) return;
     const uint64_t rp = rowptr[i];
-    const uint32_t dg = (uint32_t)(rowptr[i + 1] - rp);
-    deg[i] = (uint8_t)dg;
+    const uint64_t dg64 = rowptr[i + 1] - rp;
+    const bool hub = dg64 > d;   // served by the generic kernel: an empty ELL row
+    const uint32_t dg = hub ? 0u : (uint32_t)dg64;
+    deg[i] = hub ? kDegHub : (uint8_t)dg;
     for (uint32_t t = 0; t < d; ++t)
         ell[(((i >> 6) * (d >> 2) + (t >> 2)) * 64 + (i & 63)) * 4 + (t & 3)] = t < dg ? colidx[rp + t] : kEllNone;
 }
@@ -95,7 +97,8 @@ __global__ __launch_bounds__(256) void k_slice_width(const uint8_t* __restrict__
     const uint64_t sl = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (sl * 64 >= N) return;
     uint32_t mx = 0;
-    for (uint64_t k = sl * 64; k < N && k < sl * 64 + 64; ++k) mx = deg[k] > mx ? deg[k] : mx;
+    for (uint64_t k = sl * 64; k < N && k < sl * 64 + 64; ++k)
+        if (deg[k] != kDegHub) mx = deg[k] > mx ? deg[k] : mx;
     sw[sl] = (uint8_t)((mx + 3) / 4);
 }
 

@@ -181,3 +181,71 @@ def test_csr_full_size_skewed_2e20(oracle_mod):
         o.run()
         assert np.array_equal(gx.view(np.uint64), o.values(0).view(np.uint64))
         assert np.array_equal(gt.view(np.uint64), o.spread_trace(0).view(np.uint64))
+
+
+def hub_graph(n, seed):
+    """Power-law rows (10..12000 entries, about 15 % above 32) plus two rows above the generic
+    kernel's 8192 entries: the fast path for most rows, hub rows on the generic / big-m path."""
+    from acsim.graphs import skewed_csr
+    rowptr, colidx = skewed_csr(n, 10, 12000, seed, alpha=2.6)
+    deg = np.diff(rowptr.astype(np.int64))
+    deg[[7, n // 2]] = [9000, 8200]
+    rowptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.uint64)
+    rng = np.random.default_rng(seed + 1)
+    colidx = rng.integers(0, n, size=int(rowptr[-1])).astype(np.uint32)
+    return rowptr, colidx
+
+
+HUB = [
+    ("trimmed_clean", dict(rule="trimmed", trim=5), {}),
+    ("trimmed_clean_binned", dict(rule="trimmed", trim=5), {"ACSIM_BIN_SA": 1024}),
+    ("wmsr_clean_binned", dict(rule="wmsr", trim=5), {"ACSIM_BIN_SA": 1024}),
+    ("midpoint_loss_crash", dict(rule="midpoint", trim=5, loss_p=0.2, fault_model="crash", n_faulty=900,
+                                 crash_window=3), {}),
+    ("average_loss", dict(rule="average", trim=0, loss_p=0.3), {}),
+    ("trimmed_omit_loss", dict(rule="trimmed", trim=5, loss_p=0.3, missing_policy="omit"), {}),
+    ("trimmed_f32", dict(rule="trimmed", trim=5, dtype="f32"), {"ACSIM_BINNED": 0}),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,kw,envs", HUB, ids=[h[0] for h in HUB])
+def test_csr_hub_rows_match_oracle(oracle_mod, name, kw, envs):
+    """Power-law CSR: rows up to the compiled degree on the register / binned path, hub rows (and
+    two rows above 8192 entries) on the generic and big-m kernels in the same round."""
+    n = 20000
+    rowptr, colidx = hub_graph(n, 43)
+    deg = np.diff(rowptr.astype(np.int64))
+    assert 0 < (deg > 32).sum() <= n // 4 and deg.max() > 8192
+    cfg = Config(n_nodes=n, topology="csr", eps=1e-9, max_rounds=60, seed=47, trace_spread=True, **kw)
+    with env(**envs), acsim.Simulator(cfg, device=0, csr=(rowptr, colidx)) as g:
+        kname = g.kernel_name()
+        assert "csr" in kname and "hubs" in kname, kname
+        g.run()
+        r, x, tr = g.rounds(), g.values(0), g.spread_trace(0)
+    with oracle_mod.OracleSimulator(cfg, csr=(rowptr, colidx), threads=8) as o:
+        o.run()
+        assert np.array_equal(o.rounds(), r)
+        view = np.uint32 if x.dtype == np.float32 else np.uint64
+        assert np.array_equal(np.ascontiguousarray(o.values(0)).view(view), np.ascontiguousarray(x).view(view))
+        assert np.array_equal(o.spread_trace(0).view(np.uint64), tr.view(np.uint64))
+
+
+@pytest.mark.gpu
+def test_csr_full_size_power_law_hubs_2e20(oracle_mod):
+    """2^20 nodes, power-law degrees 11..20000 (about 19 % of the rows above 32 entries), trimmed
+    t = 5: binned CSR path for the rows up to 32, generic / big-m kernels for the hubs, 6 FIXED
+    rounds bit-exact vs the oracle."""
+    N = 1 << 20
+    rowptr, colidx = skewed_csr(N, 11, 20000, 13, alpha=2.5)
+    cfg = Config(n_nodes=N, topology="csr", rule="trimmed", trim=5, termination="fixed", max_rounds=6, seed=14,
+                 trace_spread=True)
+    with acsim.Simulator(cfg, csr=(rowptr, colidx)) as g:
+        kname = g.kernel_name()
+        g.run()
+        gx, gt = g.values(0), g.spread_trace(0)
+    assert kname.startswith("k_bin_scatter") and "hubs" in kname, kname
+    with oracle_mod.OracleSimulator(cfg, threads=16, csr=(rowptr, colidx)) as o:
+        o.run()
+        assert np.array_equal(gx.view(np.uint64), o.values(0).view(np.uint64))
+        assert np.array_equal(gt.view(np.uint64), o.spread_trace(0).view(np.uint64))

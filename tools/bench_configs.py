@@ -31,6 +31,10 @@ CASES = {
     # user graph (§8(f) row 1): 2^20 nodes, power-law degrees 11..32, hub-skewed senders, trimmed t=5
     "csr_2e20": dict(max_rounds=20),
     "csr_2e20_generic": dict(max_rounds=20),   # the same graph on the one-workgroup-per-receiver kernel
+    # power-law user graph with hubs: degrees 11..20000 (about 19 % of the rows above 32): fast path +
+    # hub rows on the generic / big-m kernels, and the same graph on the generic kernel alone
+    "csr_2e20_hubs": dict(max_rounds=10),
+    "csr_2e20_hubs_generic": dict(max_rounds=10),
     # size probes of the headline shape (stage 64 / 128 / 512 MiB against the 256 MiB MALL)
     "cfg4_n18": dict(max_rounds=100, n_nodes=1 << 18),
     "cfg4_n19": dict(max_rounds=100, n_nodes=1 << 19),
@@ -44,7 +48,7 @@ def run(name, **kw):
     csr = None
     if name.startswith("csr_2e20"):
         from acsim.graphs import skewed_csr
-        csr = skewed_csr(1 << 20, 11, 32, 11)
+        csr = skewed_csr(1 << 20, 11, 20000, 13, alpha=2.5) if "hubs" in name else skewed_csr(1 << 20, 11, 32, 11)
         cfg = acsim.Config(n_nodes=1 << 20, topology="csr", rule="trimmed", trim=5, termination="fixed", **kw)
         os.environ["ACSIM_CSR_FAST"] = "0" if name.endswith("_generic") else "1"
     elif name == "complete_16k_loss":
