@@ -122,6 +122,9 @@ struct acs_sim {
         uint64_t off, n;
         uint32_t P;
     };
+    uint32_t* crank = nullptr;     // fp32 tagged binned plans above 2^20 nodes with crash faults (RoundArgs::crank)
+    uint32_t* clist = nullptr;
+    std::vector<uint32_t> coff;    // [crash_window + 1] start of round r's crashing senders in clist
     uint32_t* gen_ids = nullptr;
     std::vector<GenClass> gcls;
     uint32_t gen_base = 0;
@@ -263,6 +266,8 @@ static void release(acs_sim* s) {
     (void)hipFree(s->deg);
     (void)hipFree(s->sw);
     (void)hipFree(s->gen_ids);
+    (void)hipFree(s->crank);
+    (void)hipFree(s->clist);
     (void)hipFree(s->dsorted);
     (void)hipFree(s->dcounts);
     (void)hipFree(s->n_done);
@@ -388,6 +393,9 @@ static RoundArgs round_args(acs_sim* s, uint32_t r) {
     a.sw = s->sw;
     a.qlo = 0;
     a.qhi = 0xFFFFFFFFu;
+    a.crank = s->crank;
+    a.clist = s->clist;
+    a.coff = s->clist && r < s->coff.size() ? s->coff[r] : 0u;
     return a;
 }
 
@@ -908,7 +916,11 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         const char* env = getenv("ACSIM_BINNED");
         const bool allow = !(env && env[0] == '0');
         const uint32_t lv = s->path == PATH_REGULAR && s->d ? binned_levels(s->N, rows_local, s->d, bin_sa, nullptr) : 0;
-        s->binned = allow && (!s->f32 || s->clean || s->N <= (1ull << 20)) && s->path == PATH_REGULAR && cfg->delay_max == 0 &&
+        // fp32 tags carry a 20-bit sender field: above 2^20 nodes a crash schedule stores crash ranks
+        // there (at most 2^20 senders may crash in one round: n_faulty <= 2^20)
+        const bool f32_tags_ok = !s->f32 || s->clean || s->N <= (1ull << 20) || cfg->fault_model != ACS_FAULT_CRASH ||
+                                 cfg->n_faulty <= (1u << 20);
+        s->binned = allow && f32_tags_ok && s->path == PATH_REGULAR && cfg->delay_max == 0 &&
                     !(s->csr_var && s->f32) &&
                     s->B == 1 && lv != 0 &&
                     binned_supported(s->d, cfg->trim, cfg->rule) && rows_local * s->d < (1ull << 32);
@@ -1007,6 +1019,27 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         CREATE_TRY(hipMalloc(&s->status, s->B * s->N * sizeof(uint32_t)));
         CREATE_TRY(build_fault_status(s->status, s->B, s->N, cfg->n_faulty, cfg->fault_model,
                                       cfg->crash_window, s->mp.key, cfg->instance_offset, s->stream));
+        if (s->binned && s->f32 && cfg->fault_model == ACS_FAULT_CRASH && s->N > (1ull << 20)) {
+            // crash ranks for the fp32 tags (RoundArgs::crank): faulty nodes grouped by crash round
+            std::vector<uint32_t> st(s->N), rank(s->N, 0u), list;
+            CREATE_TRY(hipMemcpy(st.data(), s->status, s->N * sizeof(uint32_t), hipMemcpyDeviceToHost));
+            const uint32_t W = cfg->crash_window;
+            s->coff.assign(W + 1, 0u);
+            for (uint64_t i = 0; i < s->N; ++i)
+                if (st[i] < W) ++s->coff[st[i] + 1];
+            for (uint32_t w = 0; w < W; ++w) s->coff[w + 1] += s->coff[w];
+            list.resize(s->coff[W] ? s->coff[W] : 1);
+            std::vector<uint32_t> fill(s->coff.begin(), s->coff.end() - 1);
+            for (uint64_t i = 0; i < s->N; ++i)
+                if (st[i] < W) {
+                    rank[i] = fill[st[i]] - s->coff[st[i]];
+                    list[fill[st[i]]++] = (uint32_t)i;
+                }
+            CREATE_TRY(hipMalloc(&s->crank, s->N * sizeof(uint32_t)));
+            CREATE_TRY(hipMalloc(&s->clist, list.size() * sizeof(uint32_t)));
+            CREATE_TRY(hipMemcpy(s->crank, rank.data(), s->N * sizeof(uint32_t), hipMemcpyHostToDevice));
+            CREATE_TRY(hipMemcpy(s->clist, list.data(), list.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        }
     }
     if (cfg->topology == ACS_TOPO_CSR) {
         CREATE_TRY(hipMalloc(&s->rowptr, (s->N + 1) * sizeof(uint64_t)));

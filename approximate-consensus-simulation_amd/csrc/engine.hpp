@@ -65,6 +65,12 @@ struct RoundArgs {
     // block partial slot pbase + blockIdx.x; nullptr: receiver blockIdx.x, slot = receiver
     const uint32_t* rid;
     uint32_t pbase;
+    // fp32 tagged binned plans above 2^20 nodes with crash faults: the binary32 tag of a sender
+    // crashing this round carries crank[j], its rank among the round's crashing senders, and
+    // phase B reads j = clist[coff + rank] (clist: faulty nodes by crash round; nullptr otherwise)
+    const uint32_t* crank;
+    const uint32_t* clist;
+    uint32_t coff;
 };
 
 constexpr uint32_t kEllNone = 0xFFFFFFFFu;   // padding column of a CSR row below the compiled degree

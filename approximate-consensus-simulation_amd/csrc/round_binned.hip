@@ -290,20 +290,21 @@ __global__ __launch_bounds__(kBinA) void k_bin_regroup(const VT* __restrict__ st
 constexpr uint64_t kTagBase = 0x7FF8000000000000ull;
 
 // fp32 plans use the binary32 quiet NaN 0x7FC00000 with the same payload layout in
-// its 22 payload bits: bits 0-1 mode, bits 2-21 the sender id (N <= 2^20, checked at create)
+// its 22 payload bits: bits 0-1 mode, bits 2-21 the sender id (N <= 2^20), or above 2^20 nodes the
+// sender's rank among the round's crashing senders (RoundArgs::crank / clist; only mode 2 reads it)
 constexpr uint32_t kTagBase32 = 0x7FC00000u;
 
 __device__ __forceinline__ double bin_tag_value(uint64_t j, uint64_t mode, double) {
     return __longlong_as_double((long long)(kTagBase | j << 2 | mode));
 }
-__device__ __forceinline__ float bin_tag_value(uint64_t j, uint64_t mode, float) {
-    return __uint_as_float(kTagBase32 | (uint32_t)(j << 2 | mode));
+__device__ __forceinline__ float bin_tag_value(uint64_t j, uint64_t mode, float) {   // 20-bit id field
+    return __uint_as_float(kTagBase32 | (uint32_t)((j & 0xFFFFFu) << 2 | mode));
 }
 
 template <typename VT = double>
 __global__ __launch_bounds__(256) void k_bin_tag(const VT* __restrict__ x, const uint32_t* __restrict__ status,
                                                  VT* __restrict__ xt, uint64_t N, uint32_t r,
-                                                 const InstState* __restrict__ st) {
+                                                 const InstState* __restrict__ st, const uint32_t* __restrict__ crank) {
     if (st->done) return;
     const uint64_t j = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 2;
     if (j >= N) return;
@@ -313,7 +314,9 @@ __global__ __launch_bounds__(256) void k_bin_tag(const VT* __restrict__ x, const
         if (k >= n) break;
         const uint32_t sj = status[j + k];
         const uint64_t mode = sj == kHonest ? 0 : sj == kByz ? 1 : r < sj ? 0 : r == sj ? 2 : 3;
-        xt[j + k] = mode ? bin_tag_value(j + k, mode, VT(0)) : x[j + k];
+        // (crank: fp32 above 2^20 nodes, the id field holds the rank among round r's crashing senders)
+        const uint64_t id = crank && mode == 2 ? crank[j + k] : j + k;
+        xt[j + k] = mode ? bin_tag_value(id, mode, VT(0)) : x[j + k];
     }
 }
 
@@ -508,7 +511,10 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const 
                             if ((bits >> 22) == 0x1FFu) {
                                 const uint32_t md = bits & 3u;
                                 stj = md == 1 ? kByz : md == 2 ? r : r - 1;
-                                if (md == 2) u = reinterpret_cast<const VT*>(a.xin)[(bits >> 2) & 0xFFFFFu];
+                                if (md == 2) {
+                                    const uint32_t f = (bits >> 2) & 0xFFFFFu;
+                                    u = reinterpret_cast<const VT*>(a.xin)[a.clist ? a.clist[a.coff + f] : f];
+                                }
                             }
                         }
                         bool miss;
@@ -1264,11 +1270,12 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
         float* st1 = reinterpret_cast<float*>(p.stage1);
         const float* fsrc = reinterpret_cast<const float*>(a.xin);
         if (!clean && a.status) {
-            if (!p.xtag || a.N > (1ull << 20)) return hipErrorInvalidValue;
+            // the 20-bit id field holds a sender id up to 2^20 nodes, beyond that a crash rank
+            if (!p.xtag || (a.N > (1ull << 20) && a.mp.fault == 1 && !a.crank)) return hipErrorInvalidValue;
             float* xt = reinterpret_cast<float*>(p.xtag);
             if (phases & 1)
                 hipLaunchKernelGGL(k_bin_tag<float>, dim3((unsigned)((a.N + 511) / 512)), dim3(256), 0, s, fsrc, a.status,
-                                   xt, a.N, a.r, a.st);
+                                   xt, a.N, a.r, a.st, a.crank);
             fsrc = xt;
         }
         if (phases & 1)
@@ -1319,7 +1326,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
         if (!p.xtag) return hipErrorInvalidValue;
         if (phases & 1)
             hipLaunchKernelGGL(k_bin_tag<double>, dim3((unsigned)((a.N + 511) / 512)), dim3(256), 0, s, a.xin, a.status,
-                               p.xtag, a.N, a.r, a.st);
+                               p.xtag, a.N, a.r, a.st, nullptr);
         src = p.xtag;
     }
     if (phases & 1)

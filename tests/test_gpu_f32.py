@@ -326,3 +326,30 @@ def test_f32_tagged_full_cfg4_byz_matches_per_lane():
         g.run()
         assert np.array_equal(g.rounds(), rb) and np.array_equal(g.spread_trace(0), tb)
         assert np.array_equal(g.values(0).view(np.uint32), xb.view(np.uint32))
+
+
+F32_TAGGED_BIG = {
+    # above 2^20 nodes: crash senders carry their crash rank in the tag's 20-bit field
+    "crash_trim_d16_2e21": Config(n_nodes=(1 << 21) + 4096, topology="regular", degree=16, rule="trimmed", trim=5,
+                                  fault_model="crash", n_faulty=30000, crash_window=3, loss_p=0.1,
+                                  termination="fixed", max_rounds=6, seed=48, trace_spread=True, dtype="f32"),
+    "byz_random_d32_2e21": Config(n_nodes=1 << 21, topology="regular", degree=32, rule="trimmed", trim=5,
+                                  fault_model="byzantine", n_faulty=20000, byz_strategy="random", byz_delta=0.1,
+                                  termination="fixed", max_rounds=5, seed=49, trace_spread=True, dtype="f32"),
+}
+
+
+@pytest.mark.parametrize("name", list(F32_TAGGED_BIG))
+def test_f32_tagged_above_2e20_matches_oracle(oracle_mod, name):
+    """The fp32 tagged binned exchange above 2^20 nodes (round 3): bit-exact vs the oracle."""
+    cfg = F32_TAGGED_BIG[name]
+    with acsim.Simulator(cfg, device=0) as g:
+        kb = g.kernel_name()
+        assert kb.startswith("k_bin_scatter") and ",faulty>" in kb and "f32" in kb, kb
+        g.run()
+        rb, xb, tb = g.rounds(), g.values(0), g.spread_trace(0)
+    with oracle_mod.OracleSimulator(cfg, threads=16) as o:
+        o.run()
+        assert np.array_equal(rb, o.rounds())
+        assert np.array_equal(xb.view(np.uint32), o.values(0).view(np.uint32))
+        assert np.array_equal(tb, o.spread_trace(0))
