@@ -224,7 +224,8 @@ def leg_cfg3(ctx: Ctx) -> dict:
 
 
 def leg_cfg5(ctx: Ctx, warm: int = 2, timed: int = 8) -> dict:
-    """BASELINE configs[4]: node partition with a per-round RCCL all-gather."""
+    """BASELINE configs[4]: node partition over RCCL: the chunked send / receive exchange
+    overlapping phase B and the next round's phase A, or the per-round all-gather."""
     import acsim
     from acsim.digest import sha256_values
     cfg = acsim.preset("cfg5", max_rounds=warm + timed)
@@ -259,7 +260,8 @@ def leg_cfg5(ctx: Ctx, warm: int = 2, timed: int = 8) -> dict:
         n = int(cfg.n_nodes)
         out = {"workload": f"cfg5: N=2^26 random 16-regular, trimmed t=5, FIXED; {warm} warm-up + "
                            f"{timed} timed rounds, node-partitioned over {ctx.world} rank(s)"
-                           + (" with a per-round RCCL all-gather" if ctx.world > 1 else ""),
+                           + ((" with the chunked RCCL exchange" if "xchunks" in kname
+                               else " with a per-round RCCL all-gather") if ctx.world > 1 else ""),
                "value": n * timed / dt, "unit": "node-rounds/s", "ms_per_round": dt / timed * 1e3,
                "kernel": kname, "round_kernel_ms_per_round": k_ms / max(1, k_n),
                "exchange_share": max(0.0, 1.0 - (k_ms / max(1, k_n)) / (dt / timed * 1e3)) if ctx.world > 1 else 0.0,
