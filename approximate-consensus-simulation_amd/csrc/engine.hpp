@@ -196,7 +196,7 @@ constexpr uint32_t kGenericMaxM = 8192;   // receivers with more entries take th
 // nrecv: grid over a.rid's list (0: every receiver); Pcls: the list's size class (0: from a.m)
 hipError_t launch_round_generic(const RoundArgs& a, uint64_t B, hipStream_t s, uint64_t nrecv = 0, uint32_t Pcls = 0);
 // big-m path (round_generic.hip): receivers with kGenericMaxM < m_i <= kGenericBigMaxM, entries
-// in global scratch (batches of at most kGenericBigCap entries), segmented radix sort, rule.
+// in global scratch (batches of at most kGenericBigCap entries), a per-receiver merge sort, rule.
 // kGenericBigMaxM keeps every sum of admitted values (|x| <= 1e300) finite.
 constexpr uint64_t kGenericBigMaxM = 1ull << 27;
 constexpr uint64_t kGenericBigCap = 1ull << 27;
@@ -211,8 +211,6 @@ struct GenericBig {
     void* ent = nullptr;                     // [cap] resolved entries (then tree-sum scratch)
     void* srt = nullptr;                     // [cap] sorted entries
     uint32_t* nmiss = nullptr;               // [max batch] entries left out (OMIT)
-    void* temp = nullptr;                    // hipCUB scratch
-    size_t temp_bytes = 0;
 };
 hipError_t generic_big_build(GenericBig& g, const std::vector<uint32_t>& ids, const std::vector<uint64_t>& m_of,
                              bool f32, hipStream_t s);

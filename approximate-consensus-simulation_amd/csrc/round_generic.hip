@@ -5,12 +5,11 @@
 // a power of two with +inf (§A.7; a sort network, so the sorted sequence — and therefore the
 // tree sum — is the spec's), then applies the rule with an LDS stride-halving tree sum.
 // Used for the dense cfg2 shape (N = 1024 complete, t = 341) and any odd (d, t).
-#include <hipcub/hipcub.hpp>
-
 #include <cstdlib>
 #include <mutex>
 
 #include "resolve.hpp"
+#include "sortnet.hpp"
 
 namespace acs {
 
@@ -43,6 +42,55 @@ __device__ __forceinline__ void block_bitonic_sort(VT* v, uint32_t P) {
             __syncthreads();
         }
     }
+}
+
+// Merge sort of v[0, P) in LDS for 256 <= P <= 8 * BLK (a power of two): runs of 8 sorted in
+// registers (19-comparator network), then log2(P / 8) merge-path passes between v and tmp, one
+// barrier each (a bitonic network needs log2(P)·(log2(P)+1)/2 barriered passes).  Returns the
+// buffer that holds the sorted sequence.  Values are never -0.0 or NaN, so equal values are
+// bit-identical and the result is the sorted sequence whatever the tie order.
+template <int BLK, typename VT>
+__device__ VT* block_merge_sort(VT* v, VT* tmp, uint32_t P) {
+    const uint32_t nt = P >> 3, t = threadIdx.x;
+    if (t < nt) {
+        VT r[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) r[q] = v[t * 8 + q];
+        select_sort<8>(r);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[t * 8 + q] = r[q];
+    }
+    __syncthreads();
+    VT* src = v;
+    VT* dst = tmp;
+    for (uint32_t w = 8; w < P; w <<= 1) {
+        if (t < nt) {
+            const uint32_t o0 = t * 8, s0 = o0 & ~(2 * w - 1), d = o0 - s0;
+            const VT* A = src + s0;
+            const VT* Bv = src + s0 + w;
+            // co-rank: the number i of A elements among the pair's first d outputs
+            uint32_t lo = d > w ? d - w : 0, hi = d < w ? d : w;
+            while (lo < hi) {
+                const uint32_t i = (lo + hi) >> 1;
+                if (A[i] <= Bv[d - i - 1]) lo = i + 1;
+                else hi = i;
+            }
+            uint32_t i = lo, j = d - lo;
+            VT* out = dst + o0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const bool ta = j >= w || (i < w && A[i] <= Bv[j]);
+                out[q] = ta ? A[i] : Bv[j];
+                i += ta;
+                j += !ta;
+            }
+        }
+        __syncthreads();
+        VT* sw = src;
+        src = dst;
+        dst = sw;
+    }
+    return src;
 }
 
 // Entry e of receiver i (§A.3 topology order, §A.5 drop, §A.4 / §A.6 resolution, bounded delay):
@@ -150,35 +198,41 @@ __global__ __launch_bounds__(BLK) void k_round_generic(const RoundArgs a, uint32
     } else if (a.rule != 4 && m <= 2 * a.trim) {   // OMIT: too few entries to trim, keep x_i
         res = xi;
     } else {
-        block_bitonic_sort<BLK>(sh, P);
+        // sorted sequence in srt, the other half of the LDS buffer is the window's scratch
+        VT* srt = sh;
+        if (P >= 256 && P <= 8u * BLK)
+            srt = block_merge_sort<BLK>(sh, sh + P, P);
+        else
+            block_bitonic_sort<BLK>(sh, P);
+        VT* wbuf = srt == sh ? sh + P : sh;
         const uint32_t t = a.trim, nr = m - 2 * t;
         if (a.rule == 4) {   // W-MSR: window [min(t, #below), m - min(t, #above))
-            uint32_t nl = 0, nle = 0;   // #entries < xi, #entries <= xi (sh is sorted)
+            uint32_t nl = 0, nle = 0;   // #entries < xi, #entries <= xi (srt is sorted)
             {
                 uint32_t lo_ = 0, hi_ = m;
-                while (lo_ < hi_) { const uint32_t md = (lo_ + hi_) >> 1; if (sh[md] < xi) lo_ = md + 1; else hi_ = md; }
+                while (lo_ < hi_) { const uint32_t md = (lo_ + hi_) >> 1; if (srt[md] < xi) lo_ = md + 1; else hi_ = md; }
                 nl = lo_;
                 hi_ = m;
-                while (lo_ < hi_) { const uint32_t md = (lo_ + hi_) >> 1; if (sh[md] <= xi) lo_ = md + 1; else hi_ = md; }
+                while (lo_ < hi_) { const uint32_t md = (lo_ + hi_) >> 1; if (srt[md] <= xi) lo_ = md + 1; else hi_ = md; }
                 nle = lo_;
             }
             const uint32_t ng = m - nle;
             const uint32_t wlo = nl < t ? nl : t, whi = ng < t ? ng : t, cnt = m - wlo - whi;
             uint32_t P2 = 1;
             while (P2 < cnt) P2 <<= 1;
-            VT* w = sh + P;
-            for (uint32_t k = threadIdx.x; k < P2; k += BLK) w[k] = k < cnt ? sh[wlo + k] : VT(0);
+            VT* w = wbuf;
+            for (uint32_t k = threadIdx.x; k < P2; k += BLK) w[k] = k < cnt ? srt[wlo + k] : VT(0);
             __syncthreads();
             res = block_tree_sum<BLK>(w, P2) / (VT)cnt;
         } else if (a.rule == 2) {
-            res = (sh[t] + sh[m - t - 1]) * VT(0.5);
+            res = (srt[t] + srt[m - t - 1]) * VT(0.5);
         } else {
             const uint32_t step = a.rule == 3 ? t : 1;
             const uint32_t cnt = a.rule == 3 ? (nr + t - 1) / t : nr;
             uint32_t P2 = 1;
             while (P2 < cnt) P2 <<= 1;
-            VT* w = sh + P;
-            for (uint32_t k = threadIdx.x; k < P2; k += BLK) w[k] = k < cnt ? sh[t + k * step] : VT(0);
+            VT* w = wbuf;
+            for (uint32_t k = threadIdx.x; k < P2; k += BLK) w[k] = k < cnt ? srt[t + k * step] : VT(0);
             __syncthreads();
             res = block_tree_sum<BLK>(w, P2) / (VT)cnt;
         }
@@ -192,9 +246,10 @@ __global__ __launch_bounds__(BLK) void k_round_generic(const RoundArgs a, uint32
 
 // ------------------------------------------------------------------------------ big m
 // Receivers with m_i > kGenericMaxM (complete graphs above 8192 nodes, CSR hubs; m_i <=
-// kGenericBigMaxM): the entries go to global scratch, a hipCUB segmented radix sort orders each
-// receiver's segment (sort-based rules), and one workgroup per receiver applies the rule with the
-// same stride-halving sums in global memory.  Receivers are processed in batches of at most
+// kGenericBigMaxM): the entries go to global scratch, k_big_sort orders each receiver's segment
+// (sort-based rules; LDS merge sorts of 8192-entry chunks, then merge-path passes in global
+// memory), and one workgroup per receiver applies the rule with the same stride-halving sums in
+// global memory.  Receivers are processed in batches of at most
 // GenericBig::cap entries; g.ids lists them, g.eoff[k] is the scratch offset of ids[k]'s segment.
 template <typename VT>
 __device__ __forceinline__ VT big_inst_ptrs(const RoundArgs& a, uint32_t lb, uint32_t i, const VT*& x, VT*& xo,
@@ -318,21 +373,70 @@ __global__ __launch_bounds__(kGenericBlock) void k_big_rule(const RoundArgs a, u
     }
 }
 
-namespace {
-struct SubBase {
-    uint64_t base;
-    __host__ __device__ uint64_t operator()(uint64_t v) const { return v - base; }
-};
-using BigOffIt = hipcub::TransformInputIterator<uint64_t, SubBase, const uint64_t*>;
+// Sort of each receiver's segment (one 1024-thread workgroup per receiver): chunks of kBigChunk
+// entries merge-sorted in LDS (+inf pads drop off the end), then merge-path passes over the
+// segment in global memory, ping-ponging between ent and srt so the result lands in srt.
+constexpr uint32_t kBigChunk = 8192;
+constexpr int kBigSortBlk = 1024;
 
 template <typename VT>
-hipError_t big_sort(void* temp, size_t& bytes, const VT* in, VT* out, uint64_t n, uint64_t nseg, const uint64_t* eoff_k0,
-                    uint64_t base, hipStream_t s) {
-    const BigOffIt beg(eoff_k0, SubBase{base});
-    return hipcub::DeviceSegmentedRadixSort::SortKeys(temp, bytes, in, out, (int)n, (int)nseg, beg, beg + 1, 0,
-                                                      (int)(sizeof(VT) * 8), s);
+__global__ __launch_bounds__(kBigSortBlk) void k_big_sort(const RoundArgs a, uint32_t lb,
+                                                          const uint64_t* __restrict__ eoff, uint64_t k0,
+                                                          VT* ent, VT* srt) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char bs_raw[];
+    VT* lv = reinterpret_cast<VT*>(bs_raw);   // [2 * kBigChunk]
+    if (a.st[lb].done) return;
+    const uint64_t k = k0 + blockIdx.x;
+    const uint64_t o = eoff[k] - eoff[k0], m = eoff[k + 1] - eoff[k];
+    const uint64_t nch = (m + kBigChunk - 1) / kBigChunk;
+    int np = 0;
+    while ((1ull << np) < nch) ++np;
+    VT* const bufs[2] = {ent + o, srt + o};
+    // chunk sorts write buffer (np & 1) ? ent : srt, so that np passes end in srt
+    VT* dst = bufs[(np & 1) ? 0 : 1];
+    for (uint64_t c = 0; c < nch; ++c) {
+        const uint64_t c0 = c * kBigChunk, L = m - c0 < kBigChunk ? m - c0 : kBigChunk;
+        uint32_t P = 256;
+        while (P < L) P <<= 1;
+        for (uint32_t e = threadIdx.x; e < P; e += kBigSortBlk) lv[e] = e < L ? ent[o + c0 + e] : (VT)kInf;
+        __syncthreads();
+        const VT* sorted = block_merge_sort<kBigSortBlk>(lv, lv + P, P);
+        for (uint32_t e = threadIdx.x; e < L; e += kBigSortBlk) dst[c0 + e] = sorted[e];
+        __syncthreads();
+    }
+    // merge passes: runs of w -> 2w over [0, m)
+    VT* src = dst;
+    dst = src == bufs[0] ? bufs[1] : bufs[0];
+    constexpr uint32_t E = 8;
+    for (uint64_t w = kBigChunk; w < m; w <<= 1) {
+        for (uint64_t o0 = (uint64_t)threadIdx.x * E; o0 < m; o0 += (uint64_t)kBigSortBlk * E) {
+            const uint64_t s0 = o0 / (2 * w) * (2 * w), d = o0 - s0;
+            const uint64_t la = m - s0 < w ? m - s0 : w;
+            const uint64_t lbn = m - s0 > w ? (m - s0 - w < w ? m - s0 - w : w) : 0;
+            const VT* A = src + s0;
+            const VT* Bv = src + s0 + la;
+            uint64_t lo = d > lbn ? d - lbn : 0, hi = d < la ? d : la;
+            while (lo < hi) {
+                const uint64_t i = (lo + hi) >> 1;
+                if (A[i] <= Bv[d - i - 1]) lo = i + 1;
+                else hi = i;
+            }
+            uint64_t i = lo, j = d - lo;
+            const uint64_t n = la + lbn - d < E ? la + lbn - d : E;
+            for (uint64_t q = 0; q < n; ++q) {
+                const bool ta = j >= lbn || (i < la && A[i] <= Bv[j]);
+                dst[o0 + q] = ta ? A[i] : Bv[j];
+                i += ta;
+                j += !ta;
+            }
+        }
+        __syncthreads();
+        VT* sw = src;
+        src = dst;
+        dst = sw;
+    }
 }
-}  // namespace
+
 
 hipError_t generic_big_build(GenericBig& g, const std::vector<uint32_t>& ids, const std::vector<uint64_t>& m_of,
                              bool f32, hipStream_t s) {
@@ -372,18 +476,6 @@ hipError_t generic_big_build(GenericBig& g, const std::vector<uint32_t>& ids, co
     if (e == hipSuccess) e = hipMemcpy(g.ids, ids.data(), ids.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = hipMemcpy(g.eoff, g.h_eoff.data(), g.h_eoff.size() * sizeof(uint64_t), hipMemcpyHostToDevice);
-    // sort scratch: the largest requirement over the batches
-    for (const auto& bt : g.batches) {
-        if (e != hipSuccess) break;
-        size_t bytes = 0;
-        const uint64_t n = g.h_eoff[bt.second] - g.h_eoff[bt.first];
-        e = f32 ? big_sort<float>(nullptr, bytes, nullptr, nullptr, n, bt.second - bt.first, g.eoff + bt.first,
-                                  g.h_eoff[bt.first], s)
-                : big_sort<double>(nullptr, bytes, nullptr, nullptr, n, bt.second - bt.first, g.eoff + bt.first,
-                                   g.h_eoff[bt.first], s);
-        g.temp_bytes = bytes > g.temp_bytes ? bytes : g.temp_bytes;
-    }
-    if (e == hipSuccess) e = hipMalloc(&g.temp, g.temp_bytes ? g.temp_bytes : 16);
     if (e != hipSuccess) generic_big_free(g);
     return e;
 }
@@ -394,7 +486,6 @@ void generic_big_free(GenericBig& g) {
     (void)hipFree(g.ent);
     (void)hipFree(g.srt);
     (void)hipFree(g.nmiss);
-    (void)hipFree(g.temp);
     g = GenericBig{};
 }
 
@@ -410,11 +501,9 @@ static hipError_t big_round(const GenericBig& g, const RoundArgs& a, uint64_t B,
                                g.eoff, k0, ent, g.nmiss);
             if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
             if (sorted) {
-                size_t bytes = g.temp_bytes;
-                if (hipError_t e = big_sort<VT>(g.temp, bytes, ent, srt, g.h_eoff[bt.second] - g.h_eoff[k0], nk,
-                                                g.eoff + k0, g.h_eoff[k0], s);
-                    e != hipSuccess)
-                    return e;
+                hipLaunchKernelGGL(k_big_sort<VT>, dim3((unsigned)nk), dim3(kBigSortBlk), 2 * kBigChunk * sizeof(VT), s, a,
+                                   (uint32_t)lb, g.eoff, k0, ent, srt);
+                if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
             }
             hipLaunchKernelGGL(k_big_rule<VT>, dim3((unsigned)nk), dim3(kGenericBlock), 0, s, a, (uint32_t)lb, g.ids,
                                g.eoff, k0, sorted ? (const VT*)srt : (const VT*)ent, ent, g.nmiss, g.pbase);
@@ -426,6 +515,19 @@ static hipError_t big_round(const GenericBig& g, const RoundArgs& a, uint64_t B,
 
 hipError_t launch_round_generic_big(const GenericBig& g, const RoundArgs& a, uint64_t B, hipStream_t s) {
     if (!g.n) return hipSuccess;
+    {   // 128 KiB of dynamic LDS for k_big_sort: the attribute is per device, set once per device ordinal
+        constexpr int kMaxDev = 64;
+        static std::once_flag once[kMaxDev];
+        static hipError_t status[kMaxDev];
+        int dev = 0;
+        if (hipError_t e = hipGetDevice(&dev); e != hipSuccess) return e;
+        if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
+        std::call_once(once[dev], [dev] {
+            status[dev] = hipFuncSetAttribute((const void*)k_big_sort<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              (int)(2 * kBigChunk * sizeof(double)));
+        });
+        if (status[dev] != hipSuccess) return status[dev];
+    }
     return g.f32 ? big_round<float>(g, a, B, s) : big_round<double>(g, a, B, s);
 }
 

@@ -41,6 +41,8 @@ CASES = {
     "cfg4_n21": dict(max_rounds=100, n_nodes=1 << 21),
     # big-m generic path: complete graph above 8192 nodes with loss (segmented radix sort per receiver)
     "complete_16k_loss": dict(max_rounds=3),
+    # generic LDS kernel: complete graph with loss (4096 entries per receiver)
+    "complete_4k_loss": dict(max_rounds=10),
 }
 
 
@@ -51,9 +53,9 @@ def run(name, **kw):
         csr = skewed_csr(1 << 20, 11, 20000, 13, alpha=2.5) if "hubs" in name else skewed_csr(1 << 20, 11, 32, 11)
         cfg = acsim.Config(n_nodes=1 << 20, topology="csr", rule="trimmed", trim=5, termination="fixed", **kw)
         os.environ["ACSIM_CSR_FAST"] = "0" if name.endswith("_generic") else "1"
-    elif name == "complete_16k_loss":
-        cfg = acsim.Config(n_nodes=16384, topology="complete", rule="trimmed", trim=100, loss_p=0.2,
-                           termination="fixed", **kw)
+    elif name in ("complete_16k_loss", "complete_4k_loss"):
+        cfg = acsim.Config(n_nodes=16384 if name.startswith("complete_16k") else 4096, topology="complete",
+                           rule="trimmed", trim=100, loss_p=0.2, termination="fixed", **kw)
     elif name == "cfg4_fixed14" or name.startswith("cfg4_n"):
         cfg = acsim.preset("cfg4", **kw)
     elif name.endswith("_f32"):
