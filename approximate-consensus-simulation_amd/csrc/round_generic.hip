@@ -134,7 +134,7 @@ __device__ __forceinline__ VT generic_entry(const RoundArgs& a, uint32_t lb, uin
 }
 
 // VT = double, or float in fp32 mode
-// BLK threads per workgroup: 64 for receivers of at most 64 entries (one wave), 1024 from 2048
+// BLK threads per workgroup: 64 for receivers of at most 512 entries (one wave), 1024 above 2048
 // entries (the serial sort passes of one receiver are the kernel's tail), 256 otherwise.
 template <int BLK, typename VT>
 __global__ __launch_bounds__(BLK) void k_round_generic(const RoundArgs a, uint32_t Pmax) {
@@ -557,7 +557,7 @@ hipError_t launch_round_generic(const RoundArgs& a, uint64_t B, hipStream_t s, u
         if (status[dev] != hipSuccess) return status[dev];
     }
     const dim3 grid((unsigned)(nrecv ? nrecv : a.N), (unsigned)B);
-    const int blk = P <= 64 ? 64 : P >= 2048 ? 1024 : 256;
+    const int blk = P <= 512 ? 64 : P <= 2048 ? 256 : 1024;   // (merge sort: P / 8 threads per pass)
 #define ACS_GEN_LAUNCH(BB)                                                                                         \
     {                                                                                                              \
         if (a.f32)                                                                                                 \
