@@ -89,6 +89,8 @@ struct acs_sim {
     uint32_t* n_done = nullptr;
     double* trace = nullptr;
     uint32_t* h_ndone = nullptr;   // pinned [2]
+    RunSummary* dsum = nullptr;    // acs_run's summary, folded on the device
+    RunSummary* h_sum = nullptr;   // pinned copy
     uint32_t round = 0;            // round of every unfinished instance
     bool all_done = false;
     // node partitioning: rank owns rows [rank*rows_per, (rank+1)*rows_per) ∩ [0, N)
@@ -273,6 +275,8 @@ static void release(acs_sim* s) {
     (void)hipFree(s->n_done);
     (void)hipFree(s->trace);
     if (s->h_ndone) (void)hipHostFree(s->h_ndone);
+    (void)hipFree(s->dsum);
+    if (s->h_sum) (void)hipHostFree(s->h_sum);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
 }
@@ -977,6 +981,8 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     }
     CREATE_TRY(hipMalloc(&s->n_done, sizeof(uint32_t)));
     CREATE_TRY(hipHostMalloc(&s->h_ndone, 2 * sizeof(uint32_t), hipHostMallocDefault));
+    CREATE_TRY(hipMalloc(&s->dsum, sizeof(RunSummary)));
+    CREATE_TRY(hipHostMalloc(&s->h_sum, sizeof(RunSummary), hipHostMallocDefault));
     if (cfg->trace_spread) {
         const uint64_t nt = s->B * ((uint64_t)cfg->max_rounds + 1);
         CREATE_TRY(hipMalloc(&s->trace, nt * sizeof(double)));
@@ -1235,19 +1241,19 @@ int acs_run(acs_sim* s, acs_result* out) {
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(s->stream));
     const auto t1 = std::chrono::steady_clock::now();
-    std::vector<InstState> v;
-    rc = read_states(s, v);
-    if (rc) return rc;
-    if (out) {
+    if (out) {   // the summary is folded on the device: 32 bytes back instead of B states
+        HIP_TRY(launch_run_summary(s->st, s->B, s->dsum, s->stream));
+        HIP_TRY(hipMemcpyAsync(s->h_sum, s->dsum, sizeof(RunSummary), hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        const RunSummary& r = *s->h_sum;
         memset(out, 0, sizeof *out);
         out->n_instances = s->B;
-        out->final_spread_max = -INFINITY;
-        for (const InstState& e : v) {
-            if (e.rounds > out->rounds_max) out->rounds_max = e.rounds;
-            out->n_converged += e.converged;
-            out->node_rounds += s->N * (uint64_t)e.rounds;
-            if (e.spread > out->final_spread_max) out->final_spread_max = e.spread;
-        }
+        out->rounds_max = r.rounds_max;
+        out->n_converged = (uint32_t)r.n_converged;
+        out->node_rounds = s->N * r.rounds_sum;
+        double sp;
+        memcpy(&sp, &r.spread_max_bits, sizeof sp);
+        out->final_spread_max = s->B ? sp : -INFINITY;
         out->wall_seconds = std::chrono::duration<double>(t1 - t0).count();
     }
     return ACS_OK;

@@ -127,6 +127,11 @@ hipError_t build_fault_status(uint32_t* status, uint64_t B, uint64_t N, uint32_t
 hipError_t launch_partials_from_x(const double* x, const uint32_t* status, uint64_t B, uint64_t N,
                                   double2* partial, uint32_t nblk, bool f32, hipStream_t s);
 hipError_t launch_finalize(const FinalizeArgs& a, uint64_t B, hipStream_t s);
+struct RunSummary {   // acs_run's result, folded on the device (32 bytes)
+    unsigned int rounds_max, pad;
+    unsigned long long n_converged, rounds_sum, spread_max_bits;
+};
+hipError_t launch_run_summary(const InstState* st, uint64_t B, RunSummary* out, hipStream_t s);
 
 // ---- round kernels
 // Register-resident kernel for RANDOM_REGULAR with a compiled (d, t) pair; returns

@@ -37,6 +37,46 @@ __global__ __launch_bounds__(kReduceBlock) void k_finalize(const FinalizeArgs a)
     finalize_instance<false>(a, lb);
 }
 
+// acs_run's summary over the B instance states (rounds_max, converged count, Σ rounds, max final
+// spread) folded on the device, so a run returns 32 bytes instead of copying B states to the host.
+// Spreads are >= +0.0, so their bit patterns order as unsigned integers.
+__global__ __launch_bounds__(kReduceBlock) void k_run_summary(const InstState* __restrict__ st, uint64_t B,
+                                                              RunSummary* out) {
+    uint32_t rmax = 0, conv = 0;
+    uint64_t rsum = 0, smax = 0;
+    for (uint64_t b = (uint64_t)blockIdx.x * kReduceBlock + threadIdx.x; b < B; b += (uint64_t)gridDim.x * kReduceBlock) {
+        const InstState e = st[b];
+        rmax = e.rounds > rmax ? e.rounds : rmax;
+        conv += e.converged;
+        rsum += e.rounds;
+        const uint64_t sb = (uint64_t)__double_as_longlong(e.spread);
+        smax = sb > smax ? sb : smax;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint32_t r2 = __shfl_xor(rmax, o, 64);
+        const uint64_t s2 = __shfl_xor(smax, o, 64);
+        rmax = r2 > rmax ? r2 : rmax;
+        smax = s2 > smax ? s2 : smax;
+        conv += __shfl_xor(conv, o, 64);
+        rsum += __shfl_xor(rsum, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(&out->rounds_max, rmax);
+        atomicAdd(&out->n_converged, (unsigned long long)conv);
+        atomicAdd(&out->rounds_sum, (unsigned long long)rsum);
+        atomicMax(&out->spread_max_bits, (unsigned long long)smax);
+    }
+}
+
+hipError_t launch_run_summary(const InstState* st, uint64_t B, RunSummary* out, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(out, 0, sizeof(RunSummary), s);
+    if (e != hipSuccess) return e;
+    const uint64_t g = (B + kReduceBlock - 1) / kReduceBlock;
+    hipLaunchKernelGGL(k_run_summary, dim3((unsigned)(g < 1024 ? g : 1024)), dim3(kReduceBlock), 0, s, st, B, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_partials_from_x(const double* x, const uint32_t* status, uint64_t B, uint64_t N,
                                   double2* partial, uint32_t nblk, bool f32, hipStream_t s) {
     if (f32)

@@ -14,6 +14,7 @@
 // receiver (the generic kernel) bit for bit, at O(N log^2 N + N·|R|/64) instead of
 // O(N^2 log^2 N) work per round.  Rounds in which a crash sender delivers partially (r == r_v),
 // message loss, AVERAGE and RANDOM Byzantine values keep the generic kernel.
+#include <mutex>
 #include "resolve.hpp"
 
 namespace acs {
@@ -459,16 +460,23 @@ bool dense_supported(uint32_t fault_model, uint32_t byz, uint32_t rule, uint32_t
 uint32_t dense_nblk(uint64_t N) { return (uint32_t)((N + (kDenseRecvBlock / 64) - 1) / (kDenseRecvBlock / 64)); }
 
 hipError_t launch_round_dense(const DenseArgs& a, hipStream_t s) {
-    static bool attr_set = false;
-    if (!attr_set) {
+    // >64 KiB dynamic LDS: the attribute belongs to the current device, so it is set once per
+    // device ordinal (a process may drive several devices from several threads)
+    constexpr int kMaxDev = 64;
+    static std::once_flag once[kMaxDev];
+    static hipError_t status[kMaxDev];
+    int dev = 0;
+    if (hipError_t e = hipGetDevice(&dev); e != hipSuccess) return e;
+    if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
+    std::call_once(once[dev], [dev] {
         hipError_t e = hipFuncSetAttribute((const void*)k_dense_sort, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)(kGenericMaxM * sizeof(double)));
         if (e == hipSuccess)
             e = hipFuncSetAttribute((const void*)k_dense_recv, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)(kGenericMaxM * sizeof(double)));
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+        status[dev] = e;
+    });
+    if (status[dev] != hipSuccess) return status[dev];
     hipLaunchKernelGGL(k_dense_sort, dim3(1), dim3(kDenseSortBlock), a.P * sizeof(double), s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -167,6 +167,25 @@ def test_gpu_matches_oracle(oracle_mod, name):
     assert_same(g, o)
 
 
+@pytest.mark.parametrize("cfg", [
+    preset("cfg3", n_instances=5000, max_rounds=8),                       # some instances hit the cap
+    preset("cfg3", n_instances=70000),
+    Config(n_nodes=512, topology="random_regular", degree=8, rule="trimmed_mean", trim=2, n_instances=37,
+           loss_p=0.2, eps=1e-9, max_rounds=300, seed=11),
+], ids=["cfg3_capped", "cfg3_70k", "regular_multi"])
+def test_run_summary_folded_on_device(cfg):
+    """acs_run's result (rounds_max, converged count, node-rounds, max final spread) is folded on
+    the device; it must equal the fold of the per-instance states."""
+    with acsim.Simulator(cfg, device=0) as g:
+        res = g.run()
+        rounds, conv, spread = g.rounds(), g.converged(), g.spread()
+    assert res.n_instances == cfg.n_instances
+    assert res.rounds_max == int(rounds.max())
+    assert res.n_converged == int(conv.sum())
+    assert res.node_rounds == int(cfg.n_nodes) * int(rounds.astype(np.int64).sum())
+    assert bits(np.array([res.final_spread_max]))[0] == bits(np.array([spread.max()]))[0]
+
+
 def test_cfg3_full_batch_sampled(oracle_mod):
     """1e5 instances on the GPU; a sample of instance windows re-run on the oracle through
     instance_offset (instances are independent and seeded by their global id)."""
