@@ -4,6 +4,8 @@
   python -m acsim validate --preset cfg4 --set n_nodes=4096
   python -m acsim run --preset cfg4_eps --out result.npz [--device 0] [--set key=value ...]
   python -m acsim sweep --preset cfg3 --set n_instances=1000 --grid loss_p=0.1,0.2 --out runs/
+  python -m acsim run --preset cfg4 --graph my_graph.npz --set trim=2 ...   (user CSR graph,
+      acsim or scipy.sparse .npz layout; topology and n_nodes come from the file)
 """
 from __future__ import annotations
 
@@ -46,12 +48,17 @@ def _grid(specs):
     return grid
 
 
-def validate(cfg: Config) -> int:
+def validate(cfg: Config, csr=None) -> int:
     """Host-side §A.8 validation through the library (no GPU needed: acs_create validates first)."""
     lib = _abi.load_library()
     c = cfg.to_c()
     h = C.c_void_p()
-    rc = lib.acs_create(C.byref(c), _abi.BACKEND_HIP, (C.c_int * 1)(0), 1, C.byref(h))
+    if csr is not None:
+        rp, ci = csr
+        rc = lib.acs_create_csr(C.byref(c), rp.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                ci.ctypes.data_as(C.POINTER(C.c_uint32)), 0, C.byref(h))
+    else:
+        rc = lib.acs_create(C.byref(c), _abi.BACKEND_HIP, (C.c_int * 1)(0), 1, C.byref(h))
     if rc == _abi.OK:
         lib.acs_destroy(h)
         return 0
@@ -71,6 +78,7 @@ def main(argv=None) -> int:
         p.add_argument("--preset", default="cfg1", choices=sorted(PRESETS))
         p.add_argument("--set", action="append", metavar="FIELD=VALUE")
         p.add_argument("--device", type=int, default=0)
+        p.add_argument("--graph", metavar="FILE.npz", help="user CSR graph (acsim.graphs.load_csr)")
         if name in ("run", "sweep"):
             p.add_argument("--out")
         if name == "sweep":
@@ -81,22 +89,27 @@ def main(argv=None) -> int:
             print(k, json.dumps(dataclasses.asdict(v)))
         return 0
     cfg = _apply(preset(a.preset), a.set)
+    csr = None
+    if a.graph:
+        from .graphs import load_csr
+        csr = load_csr(a.graph)
+        cfg = cfg.replace(topology="csr", n_nodes=int(csr[0].size - 1))
     if a.cmd == "validate":
-        rc = validate(cfg)
+        rc = validate(cfg, csr)
         if rc == 0:
             print("ok")
         return rc
     if a.cmd == "run":
         from .io import save_result
         from .sim import simulate
-        res = simulate(cfg, device=a.device, return_values=bool(a.out))
+        res = simulate(cfg, device=a.device, return_values=bool(a.out), csr=csr)
         from .sweep import summarize
         print(json.dumps(summarize(cfg, res)))
         if a.out:
             save_result(a.out, res, cfg)
         return 0
     from .sweep import sweep
-    rows = sweep(cfg, _grid(a.grid), out_dir=a.out, device=a.device)
+    rows = sweep(cfg, _grid(a.grid), out_dir=a.out, device=a.device, csr=csr)
     for r in rows:
         print(json.dumps(r))
     return 0

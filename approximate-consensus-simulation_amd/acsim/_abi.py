@@ -97,6 +97,10 @@ class AcsError(RuntimeError):
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG_DIR, "_lib", "libacsim.so")
+# experiments only: a variant build of the same sources (Makefile OUTDIR / XFLAGS), e.g. a
+# different compile-time receiver-block size; the product loads the in-tree default
+if os.environ.get("ACSIM_LIB"):
+    LIB_PATH = os.environ["ACSIM_LIB"]
 
 _lib = None
 

@@ -38,11 +38,13 @@ def summarize(cfg: Config, res) -> Dict:
 
 
 def sweep(base: Config, grid: Dict[str, Iterable], out_dir: Optional[str] = None, device: int = 0,
-          run: Optional[Callable] = None, keep_values: bool = False) -> List[Dict]:
-    """run(cfg) -> Result (default: acsim.simulate on `device`)."""
+          run: Optional[Callable] = None, keep_values: bool = False, csr=None) -> List[Dict]:
+    """run(cfg) -> Result (default: acsim.simulate on `device`; csr: a user graph for
+    topology="csr" configs, shared by every point)."""
     if run is None:
         from .sim import simulate
-        run = lambda c: simulate(c, device=device, return_values=keep_values or out_dir is not None)  # noqa: E731
+        run = lambda c: simulate(c, device=device, return_values=keep_values or out_dir is not None,  # noqa: E731
+                                 csr=csr)
     rows = []
     if out_dir:
         os.makedirs(out_dir, exist_ok=True)

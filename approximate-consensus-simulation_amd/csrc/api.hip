@@ -915,7 +915,8 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     // multiset), ACSIM_BIN_OF=1: measured slower than the invpos phase B, kept as
     // a tested variant
     const char* of_env = getenv("ACSIM_BIN_OF");
-    const bool bin_of = s->ell_sorted && of_env && of_env[0] == '1' && !s->csr_var;
+    // (rid is one byte per entry: receiver blocks of at most 256)
+    const bool bin_of = s->ell_sorted && of_env && of_env[0] == '1' && !s->csr_var && kBinSB <= 256;
     {
         const char* env = getenv("ACSIM_BINNED");
         const bool allow = !(env && env[0] == '0');

@@ -148,7 +148,10 @@ constexpr uint32_t kRegularBlock = 256;
 // for two-level plans phase M regroups stage1 by receiver block into stage2; phase B (one
 // receiver block per workgroup) copies its runs into LDS by LDS-DMA, then every lane reads its d
 // values through invpos and applies the rule in registers.
-constexpr uint32_t kBinSB = 256;        // receivers per phase-B workgroup (one lane each)
+#ifndef ACS_BIN_SB
+#define ACS_BIN_SB 256
+#endif
+constexpr uint32_t kBinSB = ACS_BIN_SB;   // receivers per phase-B workgroup (one lane each)
 struct BinnedPlan {
     uint32_t D = 0, SA = 0, P = 0, Q = 0, levels = 0, PK = 0, ngroups = 0, nrun = 0, mcap = 0;
     bool f32 = false;                   // fp32 plan (float stage, runs padded to 4 elements)
