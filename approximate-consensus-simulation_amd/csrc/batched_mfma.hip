@@ -63,13 +63,7 @@ __global__ __launch_bounds__(64) void k_batched_mfma(const BatchArgs a, uint32_t
         uint64_t miss = 0;
         if (mp.thr && lane < N) {
             if ((N & 3u) == 0) {
-                const uint32_t nq = N >> 2;
-                for (uint32_t g = 0; g < nq; ++g) {
-                    const U4 w = philox10(lane * nq + g, R, bG, kStreamDrop, mp.key);
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        if (w.v[e] < mp.thr) miss |= 1ull << (4 * g + e);
-                }
+                miss = drop_mask_n4(lane, N >> 2, R, bG, mp.key, mp.thr);
             } else {
                 for (uint32_t j = 0; j < N; ++j)
                     if (draw(mp.key, kStreamDrop, bG, R, (uint64_t)lane * N + j) < mp.thr) miss |= 1ull << j;

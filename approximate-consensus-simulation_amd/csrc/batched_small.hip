@@ -182,13 +182,7 @@ __global__ __launch_bounds__(64) void k_batched_small(const BatchArgs a, uint32_
         // drop mask (§A.5): slot s = lane*N + j
         if (mp.thr && act) {
             if ((N & 3u) == 0) {
-                const uint32_t nq = N >> 2;
-                for (uint32_t g = 0; g < nq; ++g) {
-                    const U4 w = philox10(lane * nq + g, r, bG, kStreamDrop, mp.key);
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        if (w.v[e] < mp.thr) c.miss |= 1ull << (4 * g + e);
-                }
+                c.miss = drop_mask_n4(lane, N >> 2, r, bG, mp.key, mp.thr);
             } else {
                 for (uint32_t j = 0; j < N; ++j)
                     if (draw(mp.key, kStreamDrop, bG, r, (uint64_t)lane * N + j) < mp.thr) c.miss |= 1ull << j;

@@ -56,7 +56,14 @@ ACS_HD U4 philox10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, Key key) 
         const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
         const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
 #endif
+#if defined(__HIP_DEVICE_COMPILE__)
+        // gfx950 v_bitop3_b32 with the XOR3 truth table (0x96): one VALU op per output word
+        // instead of two v_xor_b32 (gfx950 has no v_xor3_b32); 20 fewer per call
+        const uint32_t n0 = __builtin_amdgcn_bitop3_b32(hi1, c1, k0, 0x96);
+        const uint32_t n2 = __builtin_amdgcn_bitop3_b32(hi0, c3, k1, 0x96);
+#else
         const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+#endif
         c0 = n0;
         c1 = lo1;
         c2 = n2;
@@ -78,6 +85,30 @@ ACS_HD uint32_t pick(const U4& w, uint32_t sel) {
 ACS_HD uint32_t draw(Key key, uint32_t stream, uint32_t b, uint32_t r, uint64_t s) {
     const U4 w = philox10((uint32_t)(s >> 2), r, b, stream, key);
     return pick(w, (uint32_t)(s & 3u));
+}
+
+// §A.5 drop mask of receiver `row` of a complete-graph instance with N = 4*nq <= 64 nodes:
+// bit j set when the message on slot row*N + j is dropped (draw < thr), one Philox call per 4
+// slots.  Each bit is shifted in from the right (m = 2m + (w < thr): a compare and two cheap ops
+// per draw instead of a 64-bit shift, select and or), so draw j of a 32-draw half lands at bit
+// (n - 1 - j); one bit reverse per half restores bit j.
+__device__ __forceinline__ uint64_t drop_mask_n4(uint32_t row, uint32_t nq, uint32_t r, uint32_t bG, Key key,
+                                                 uint32_t thr) {
+    const uint32_t n0 = nq < 8u ? nq : 8u;
+    uint32_t m0 = 0, m1 = 0;
+    for (uint32_t g = 0; g < n0; ++g) {
+        const U4 w = philox10(row * nq + g, r, bG, kStreamDrop, key);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) m0 = m0 + m0 + (uint32_t)(w.v[e] < thr);
+    }
+    for (uint32_t g = 8; g < nq; ++g) {
+        const U4 w = philox10(row * nq + g, r, bG, kStreamDrop, key);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) m1 = m1 + m1 + (uint32_t)(w.v[e] < thr);
+    }
+    const uint32_t b0 = __builtin_bitreverse32(m0) >> (32u - 4u * n0);
+    const uint32_t b1 = nq > 8u ? __builtin_bitreverse32(m1) >> (32u - 4u * (nq - 8u)) : 0u;
+    return (uint64_t)b1 << 32 | b0;
 }
 
 // §A.1 u53(w0, w1) = ((w0>>5)·2^26 + (w1>>6)) · 2^-53  (exact)
