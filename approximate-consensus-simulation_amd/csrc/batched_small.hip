@@ -108,14 +108,21 @@ __device__ __forceinline__ VT average_tree(const LaneCtx<VT>& c, std::integer_se
 // Bit-select of two values of the same width: (m & a) | (~m & b) per 32-bit word (v_bfi_b32), m all
 // ones or all zeros.  No lane-mask (SGPR pair) per entry: 64 entries' compare masks held live
 // otherwise spill SGPRs to VGPR lanes.
+// v_bfi_b32 written out: given a mask it can prove is 0 / -1 the compiler turns the and/or form
+// into a compare plus two v_cndmask per value (one VALU op more per leaf).
+__device__ __forceinline__ uint32_t bfi32(uint32_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+}
 __device__ __forceinline__ double bitsel(uint32_t m, double a, double b) {
     const uint64_t ua = (uint64_t)__double_as_longlong(a), ub = (uint64_t)__double_as_longlong(b);
-    const uint32_t lo = (m & (uint32_t)ua) | (~m & (uint32_t)ub);
-    const uint32_t hi = (m & (uint32_t)(ua >> 32)) | (~m & (uint32_t)(ub >> 32));
+    const uint32_t lo = bfi32(m, (uint32_t)ua, (uint32_t)ub);
+    const uint32_t hi = bfi32(m, (uint32_t)(ua >> 32), (uint32_t)(ub >> 32));
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 __device__ __forceinline__ float bitsel(uint32_t m, float a, float b) {
-    return __uint_as_float((m & __float_as_uint(a)) | (~m & __float_as_uint(b)));
+    return __uint_as_float(bfi32(m, __float_as_uint(a), __float_as_uint(b)));
 }
 
 // AVERAGE without a fault schedule (cfg3): entry j is x_i when bit j of `usexi` is set (missing
@@ -132,8 +139,9 @@ __device__ __forceinline__ VT average_tree_sel(const VT* xs, VT xi, uint64_t use
     auto leaf = [&](int j) -> VT {
         if (!FULL && j >= (int)N) return VT(0);
         VT v = xs[j];
-        if constexpr (OMIT) v = bitsel(0u - (((j < 32 ? z0 : z1) >> (j & 31)) & 1u), VT(0), v);
-        return bitsel(0u - (((j < 32 ? w0 : w1) >> (j & 31)) & 1u), xi, v);
+        // all-ones / all-zeros select mask of bit j: one signed 1-bit field extract (v_bfe_i32)
+        if constexpr (OMIT) v = bitsel((uint32_t)__builtin_amdgcn_sbfe((int)(j < 32 ? z0 : z1), j & 31, 1), VT(0), v);
+        return bitsel((uint32_t)__builtin_amdgcn_sbfe((int)(j < 32 ? w0 : w1), j & 31, 1), xi, v);
     };
     // scheduling fence every 8 leaves: unfenced, the compiler hoists all 64 LDS reads (128 VGPRs
     // live, one wave per SIMD); fenced, a group's reads overlap only the previous group's adds
