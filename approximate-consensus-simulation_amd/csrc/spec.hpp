@@ -92,6 +92,18 @@ ACS_HD uint32_t draw(Key key, uint32_t stream, uint32_t b, uint32_t r, uint64_t 
 // slots.  Each bit is shifted in from the right (m = 2m + (w < thr): a compare and two cheap ops
 // per draw instead of a 64-bit shift, select and or), so draw j of a 32-draw half lands at bit
 // (n - 1 - j); one bit reverse per half restores bit j.
+// m = 2m + (w < thr) as v_cmp (borrow into vcc) + v_addc (m + m + vcc).  Written out: the compiler
+// turns the add into an or of disjoint bits and spends a v_cndmask plus a share of a v_or3 per draw.
+// (The s_nop covers the VALU vcc write -> VALU vcc read distance; thr is uniform, an SGPR.)
+__device__ __forceinline__ uint32_t shift_in_lt(uint32_t m, uint32_t w, uint32_t thr) {
+    uint32_t out;
+    asm("v_cmp_gt_u32 vcc, %2, %1\n\ts_nop 1\n\tv_addc_co_u32 %0, vcc, %3, %3, vcc"
+        : "=v"(out)
+        : "v"(w), "s"(thr), "v"(m)
+        : "vcc");
+    return out;
+}
+
 __device__ __forceinline__ uint64_t drop_mask_n4(uint32_t row, uint32_t nq, uint32_t r, uint32_t bG, Key key,
                                                  uint32_t thr) {
     const uint32_t n0 = nq < 8u ? nq : 8u;
@@ -99,12 +111,12 @@ __device__ __forceinline__ uint64_t drop_mask_n4(uint32_t row, uint32_t nq, uint
     for (uint32_t g = 0; g < n0; ++g) {
         const U4 w = philox10(row * nq + g, r, bG, kStreamDrop, key);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) m0 = m0 + m0 + (uint32_t)(w.v[e] < thr);
+        for (int e = 0; e < 4; ++e) m0 = shift_in_lt(m0, w.v[e], thr);
     }
     for (uint32_t g = 8; g < nq; ++g) {
         const U4 w = philox10(row * nq + g, r, bG, kStreamDrop, key);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) m1 = m1 + m1 + (uint32_t)(w.v[e] < thr);
+        for (int e = 0; e < 4; ++e) m1 = shift_in_lt(m1, w.v[e], thr);
     }
     const uint32_t b0 = __builtin_bitreverse32(m0) >> (32u - 4u * n0);
     const uint32_t b1 = nq > 8u ? __builtin_bitreverse32(m1) >> (32u - 4u * (nq - 8u)) : 0u;
