@@ -77,7 +77,7 @@ def parse():
                         "stream ~5 us, so sampling keeps the timed region representative)")
     p.add_argument("--legs", default="cfg3,cfg5",
                    help="comma-separated extra legs (cfg3, cfg5); empty for none")
-    p.add_argument("--leg-timeout", type=float, default=420.0,
+    p.add_argument("--leg-timeout", type=float, default=180.0,
                    help="watchdog: print the line without the unfinished legs after this many seconds")
     p.add_argument("--allow-shared-device", action="store_true",
                    help="rehearsal only: run more ranks than GPUs (n_gpus then counts distinct devices "
