@@ -1,0 +1,193 @@
+"""Property-based differential tests over the whole configuration space (SURVEY §4 rows L0 and L2,
+hypothesis).  The fixed-case tests pin chosen corners; these draw random small configurations —
+topology, degree, rule and trim, fault model and strategy, loss, delay, missing policy, instances,
+dtype, termination, seeds — and check:
+
+  CPU  the C oracle against the independent numpy restatement, bit for bit (rounds, every value,
+       every spread trace), and two semantic properties of the rules:
+         validity     without Byzantine senders every value stays inside the hull of x^0 (up to
+                      the rounding of one mean: a few ulps),
+         contraction  without faults and delays the honest spread never grows (same tolerance;
+                      with delays only the hull of the last D+1 rounds contracts);
+  GPU  the HIP path (libacsim.so, through the C ABI) against the oracle on the same draws, bit for
+       bit (every draw avoids the MFMA path, whose bar is 1e-12).
+
+Draws are derandomized (a fixed example sequence), so a failure reproduces; the failing Config is
+printed by hypothesis.  Parity is against the frozen spec (no upstream code exists).
+"""
+import numpy as np
+import pytest
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+import spec_np as S
+from acsim.config import Config
+
+
+@st.composite
+def configs(draw, max_n=160):
+    """A valid small Config (acs_create's admission rules, include/acsim.h)."""
+    topo = draw(st.sampled_from(["complete", "random_regular"]))
+    if topo == "complete":
+        n = draw(st.integers(3, 40))
+        d = 0
+        m = n
+    else:
+        n = draw(st.integers(8, max_n))
+        d = draw(st.sampled_from([2, 4, 6, 8, 12, 16]))
+        m = d + 1
+    rule = draw(st.sampled_from(["average", "trimmed", "midpoint", "dlpsw", "wmsr"]))
+    tmax = (m - 1) // 2
+    if rule == "average":
+        t = 0
+    elif rule == "dlpsw":
+        if tmax < 1:
+            rule, t = "trimmed", 0
+        else:
+            t = draw(st.integers(1, tmax))
+    else:
+        t = draw(st.integers(0, tmax))
+    fault = draw(st.sampled_from(["none", "none", "crash", "byzantine"]))
+    kw = {}
+    if fault != "none":
+        kw["n_faulty"] = draw(st.integers(1, max(1, n // 4)))
+    if fault == "crash":
+        kw["crash_window"] = draw(st.integers(1, 6))
+    if fault == "byzantine":
+        kw["byz_strategy"] = draw(st.sampled_from(["split", "random", "constant"]))
+        kw["byz_delta"] = draw(st.sampled_from([0.0, 0.05, 0.5]))
+        kw["byz_const"] = draw(st.sampled_from([0.0, -2.0, 7.5]))
+    dtype = draw(st.sampled_from(["f64", "f64", "f32"]))
+    term = draw(st.sampled_from(["eps", "fixed"]))
+    return Config(
+        n_nodes=n, n_instances=draw(st.integers(1, 3)), topology=topo, degree=d, rule=rule, trim=t,
+        fault_model=fault, loss_p=draw(st.sampled_from([0.0, 0.0, 0.1, 0.35])),
+        mask_group=draw(st.sampled_from([1, 1, 2])), eps=draw(st.sampled_from([1e-4, 1e-7, 1e-10])),
+        max_rounds=draw(st.integers(1, 60)), termination=term, dtype=dtype,
+        seed=draw(st.integers(0, 2 ** 40)), graph_seed=draw(st.sampled_from([0, 0, 5])),
+        trace_spread=True, instance_offset=draw(st.sampled_from([0, 0, 1000])),
+        delay_max=draw(st.sampled_from([0, 0, 0, 1, 3])),
+        missing_policy=draw(st.sampled_from(["self", "self", "omit"])), **kw)
+
+
+@st.composite
+def csr_configs(draw, max_n=300):
+    """A user graph (ACS_TOPO_CSR, §8(f) row 1) with random degrees and senders, and a valid
+    Config for it: (cfg, (rowptr, colidx))."""
+    n = draw(st.integers(8, max_n))
+    dmin = draw(st.integers(1, 12))
+    dmax = dmin + draw(st.sampled_from([0, 3, 20, 60]))
+    rng = np.random.default_rng(draw(st.integers(0, 2 ** 32)))
+    deg = rng.integers(dmin, dmax + 1, size=n)
+    rowptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.uint64)
+    colidx = rng.integers(0, n, size=int(rowptr[-1])).astype(np.uint32)
+    base = draw(configs())
+    tmax = dmin // 2   # m_i = deg(i) + 1 > 2t for every row
+    rule = base.rule
+    t = 0 if rule == "average" else draw(st.integers(1 if rule == "dlpsw" else 0, max(tmax, 1)))
+    if t > tmax:
+        rule, t = "average", 0
+    cfg = base.replace(topology="csr", n_nodes=n, degree=0, rule=rule, trim=t,
+                       n_faulty=min(base.n_faulty, n - 1))
+    return cfg, (rowptr, colidx)
+
+
+def _run_oracle(oracle_mod, cfg, csr=None):
+    with oracle_mod.OracleSimulator(cfg, csr=csr) as o:
+        o.run()
+        return dict(rounds=o.rounds(), x=o.all_values(), status=o.fault_status(),
+                    trace=[o.spread_trace(b) for b in range(cfg.n_instances)])
+
+
+def _bits(a):
+    a = np.ascontiguousarray(a)
+    return a.view(np.uint32 if a.dtype == np.float32 else np.uint64)
+
+
+CPU_SETTINGS = settings(max_examples=150, deadline=None, derandomize=True, database=None,
+                        suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+
+
+@CPU_SETTINGS
+@given(cfg=configs())
+def test_oracle_matches_numpy_random_configs(oracle_mod, cfg):
+    o = _run_oracle(oracle_mod, cfg)
+    n = S.NpSim(cfg)
+    n.run()
+    assert np.array_equal(o["rounds"], n.rounds), cfg
+    assert np.array_equal(_bits(o["x"]), _bits(n.x)), cfg
+    for b in range(cfg.n_instances):
+        assert np.array_equal(_bits(o["trace"][b]), _bits(np.array(n.trace[b]))), (cfg, b)
+
+
+@settings(CPU_SETTINGS, max_examples=25)   # the numpy CSR restatement loops per row
+@given(case=csr_configs(max_n=120))
+def test_oracle_matches_numpy_random_csr(oracle_mod, case):
+    cfg, csr = case
+    o = _run_oracle(oracle_mod, cfg, csr)
+    n = S.NpSim(cfg, csr=csr)
+    n.run()
+    assert np.array_equal(o["rounds"], n.rounds), cfg
+    assert np.array_equal(_bits(o["x"]), _bits(n.x)), cfg
+    for b in range(cfg.n_instances):
+        assert np.array_equal(_bits(o["trace"][b]), _bits(np.array(n.trace[b]))), (cfg, b)
+
+
+def _x0(oracle_mod, cfg):
+    with oracle_mod.OracleSimulator(cfg.replace(max_rounds=1, termination="fixed")) as o:
+        o.round(0)
+        return o.all_values()
+
+
+@CPU_SETTINGS
+@given(cfg=configs())
+def test_validity_and_contraction(oracle_mod, cfg):
+    if cfg.fault_model == "byzantine":
+        return   # Byzantine values may lie outside the hull by design (§A.4)
+    x0 = _x0(oracle_mod, cfg).astype(np.float64)
+    o = _run_oracle(oracle_mod, cfg)
+    ulp = np.float64(np.finfo(np.float32 if cfg.dtype == "f32" else np.float64).eps)
+    for b in range(cfg.n_instances):
+        lo, hi = x0[b].min(), x0[b].max()
+        tol = 8 * ulp * max(abs(lo), abs(hi), 1.0)
+        xb = o["x"][b].astype(np.float64)
+        assert xb.min() >= lo - tol and xb.max() <= hi + tol, (cfg, b)
+        if cfg.fault_model == "none" and cfg.delay_max == 0:
+            tr = np.asarray(o["trace"][b], dtype=np.float64)
+            assert np.all(np.diff(tr) <= tol), (cfg, b, tr)
+
+
+@pytest.mark.gpu
+@settings(max_examples=300, deadline=None, derandomize=True, database=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+@given(cfg=configs(max_n=400))
+def test_gpu_matches_oracle_random_configs(oracle_mod, cfg):
+    import acsim
+    with acsim.Simulator(cfg, device=0) as g:
+        g.run()
+        gr, gx, gs = g.rounds(), g.all_values(), g.fault_status()
+        gt = [g.spread_trace(b) for b in range(cfg.n_instances)]
+    o = _run_oracle(oracle_mod, cfg)
+    assert np.array_equal(gr, o["rounds"]), cfg
+    assert np.array_equal(gs, o["status"]), cfg
+    assert np.array_equal(_bits(gx), _bits(o["x"])), cfg
+    for b in range(cfg.n_instances):
+        assert np.array_equal(_bits(gt[b]), _bits(o["trace"][b])), (cfg, b)
+
+
+@pytest.mark.gpu
+@settings(max_examples=200, deadline=None, derandomize=True, database=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+@given(case=csr_configs(max_n=600))
+def test_gpu_matches_oracle_random_csr(oracle_mod, case):
+    import acsim
+    cfg, csr = case
+    with acsim.Simulator(cfg, device=0, csr=csr) as g:
+        g.run()
+        gr, gx = g.rounds(), g.all_values()
+        gt = [g.spread_trace(b) for b in range(cfg.n_instances)]
+    o = _run_oracle(oracle_mod, cfg, csr)
+    assert np.array_equal(gr, o["rounds"]), cfg
+    assert np.array_equal(_bits(gx), _bits(o["x"])), cfg
+    for b in range(cfg.n_instances):
+        assert np.array_equal(_bits(gt[b]), _bits(o["trace"][b])), (cfg, b)
