@@ -191,3 +191,59 @@ def test_gpu_matches_oracle_random_csr(oracle_mod, case):
     assert np.array_equal(_bits(gx), _bits(o["x"])), cfg
     for b in range(cfg.n_instances):
         assert np.array_equal(_bits(gt[b]), _bits(o["trace"][b])), (cfg, b)
+
+
+@st.composite
+def binned_configs(draw):
+    """One-instance RANDOM_REGULAR configs the binned exchange serves (compiled (d, t) pairs, no
+    delays), at sizes that span many source blocks when ACSIM_BIN_SA shrinks them: one-level and
+    two-level (phase-M) plans, ragged last blocks, clean / lossy / crash / Byzantine senders, every
+    sort-based rule and AVERAGE, fp64 and fp32, SELF and OMIT.  -> (cfg, source block size)"""
+    d, t = draw(st.sampled_from([(8, 0), (8, 2), (16, 0), (16, 5), (32, 0), (32, 5)]))
+    rule = draw(st.sampled_from(["trimmed", "midpoint", "wmsr", "dlpsw"] if t else
+                                ["average", "trimmed", "midpoint"]))
+    fault = draw(st.sampled_from(["none", "none", "crash", "byzantine"]))
+    n = draw(st.integers(3000, 120000))
+    kw = {}
+    if fault != "none":
+        kw["n_faulty"] = draw(st.integers(1, n // 50))
+    if fault == "crash":
+        kw["crash_window"] = draw(st.integers(1, 6))
+    if fault == "byzantine":
+        kw["byz_strategy"] = draw(st.sampled_from(["split", "random", "constant"]))
+        kw["byz_delta"] = draw(st.sampled_from([0.0, 0.05]))
+        kw["byz_const"] = draw(st.sampled_from([0.0, 3.0]))
+    cfg = Config(n_nodes=n, topology="random_regular", degree=d, rule=rule, trim=t, fault_model=fault,
+                 loss_p=draw(st.sampled_from([0.0, 0.0, 0.1])), eps=draw(st.sampled_from([1e-7, 1e-10])),
+                 max_rounds=draw(st.integers(1, 40)), termination=draw(st.sampled_from(["eps", "fixed"])),
+                 dtype=draw(st.sampled_from(["f64", "f64", "f32"])), seed=draw(st.integers(0, 2 ** 40)),
+                 trace_spread=True, missing_policy=draw(st.sampled_from(["self", "self", "omit"])), **kw)
+    return cfg, draw(st.sampled_from([256, 512, 1024, 4096]))
+
+
+@pytest.mark.gpu
+@settings(max_examples=120, deadline=None, derandomize=True, database=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+@given(case=binned_configs())
+def test_gpu_binned_exchange_random_configs(oracle_mod, case):
+    """The binned exchange (round_binned.hip) with small source blocks against the oracle."""
+    import os
+    import acsim
+    cfg, sa = case
+    old = os.environ.get("ACSIM_BIN_SA")
+    os.environ["ACSIM_BIN_SA"] = str(sa)
+    try:
+        with acsim.Simulator(cfg, device=0) as g:
+            name = g.kernel_name()
+            g.run()
+            gr, gx, gt = g.rounds(), g.values(0), g.spread_trace(0)
+    finally:
+        if old is None:
+            os.environ.pop("ACSIM_BIN_SA", None)
+        else:
+            os.environ["ACSIM_BIN_SA"] = old
+    assert "k_bin_" in name, (cfg, sa, name)   # the draw must land on the binned exchange
+    o = _run_oracle(oracle_mod, cfg.replace(omp_threads=16))
+    assert np.array_equal(gr, o["rounds"]), (cfg, sa, name)
+    assert np.array_equal(_bits(gx), _bits(o["x"][0])), (cfg, sa, name)
+    assert np.array_equal(_bits(gt), _bits(o["trace"][0])), (cfg, sa, name)
