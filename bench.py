@@ -24,6 +24,9 @@ sample of the same workload.
 
 Extra legs (every N, each guarded: a failing leg is reported as an error string and never costs
 the headline line; a watchdog prints the line if a leg hangs):
+  cfg4_f32          the headline workload in fp32 mode (north_star: "fp32 mode stated
+                    separately"), timed and roofline-priced like the headline at 264 B/node-round,
+                    100 FIXED rounds of a fresh handle checked against the oracle's hash.
   cfg3_sharded      10^5 instances x 64 nodes (BASELINE configs[2]) sharded over the ranks by
                     contiguous global instance blocks, no data-path collective; node-rounds/s
                     of the whole job (the batch run 4 times back to back per rank, so the
@@ -75,8 +78,8 @@ def parse():
     p.add_argument("--event-every", type=int, default=10,
                    help="bracket every k-th timed round with HIP events (each pair idles the "
                         "stream ~5 us, so sampling keeps the timed region representative)")
-    p.add_argument("--legs", default="cfg3,cfg5",
-                   help="comma-separated extra legs (cfg3, cfg5); empty for none")
+    p.add_argument("--legs", default="f32,cfg3,cfg5",
+                   help="comma-separated extra legs (f32, cfg3, cfg5); empty for none")
     p.add_argument("--leg-timeout", type=float, default=180.0,
                    help="watchdog: print the line without the unfinished legs after this many seconds")
     p.add_argument("--allow-shared-device", action="store_true",
@@ -287,7 +290,42 @@ def leg_cfg5(ctx: Ctx, warm: int = 2, timed: int = 8) -> dict:
     return out
 
 
-LEGS = {"cfg3": ("cfg3_sharded", leg_cfg3), "cfg5": ("cfg5_partitioned", leg_cfg5)}
+def leg_cfg4_f32(ctx: Ctx, warm: int = 10, timed: int = 100) -> dict:
+    """fp32 mode of the headline workload (BASELINE.json north_star: "fp32 mode stated separately",
+    DESIGN.md §9): cfg4 in binary32, timed and roofline-priced like the headline (264 B/node-round,
+    SURVEY §8(d)); a fresh handle's 100 FIXED rounds are checked against the oracle's hash."""
+    import acsim
+    from acsim.digest import sha256_values
+    cfg = acsim.preset("cfg4", max_rounds=warm + timed, instance_offset=ctx.rank, dtype="f32")
+    with acsim.Simulator(cfg, device=ctx.dev) as sim:
+        sim.round(warm)
+        sim.set_kernel_timing(True, every=10)
+        ctx.barrier(sim)
+        t0 = time.perf_counter()
+        sim.round(timed)
+        ctx.barrier(sim)
+        dt = ctx.max(time.perf_counter() - t0)
+        k_ms, k_n, kname = sim.kernel_timing()
+    n = int(cfg.n_nodes)
+    avg_s = (k_ms / 1e3 / k_n) if k_n else dt / timed
+    out = {}
+    if ctx.rank == 0:
+        with acsim.Simulator(acsim.preset("cfg4", max_rounds=100, dtype="f32"), device=ctx.dev) as chk:
+            chk.run()
+            ok = sha256_values(chk.values(0)) == golden().get("cfg4", {}).get("f32_fixed100_x_sha256")
+        achieved = BYTES_PER_NODE_ROUND_F32 * n / avg_s / 1e9
+        out = {"workload": "cfg4 in fp32 mode (binary32 values, DESIGN.md §9), FIXED rounds",
+               "value": ctx.world * n * timed / dt, "unit": "node-rounds/s", "ms_per_step": dt / timed * 1e3,
+               "dtype": "f32", "kernel": kname, "avg_launch_us": avg_s * 1e6,
+               "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": achieved / HBM_PEAK_GBS, "bytes_per_node_round": BYTES_PER_NODE_ROUND_F32,
+                            "traffic": load_pmc(kname, n, "f32")},
+               "golden_match": ok}
+    return out
+
+
+LEGS = {"cfg3": ("cfg3_sharded", leg_cfg3), "cfg5": ("cfg5_partitioned", leg_cfg5),
+        "f32": ("cfg4_f32", leg_cfg4_f32)}
 
 
 def main():

@@ -12,7 +12,11 @@ What is hashed (the GPU tests and bench.py's multi-GPU legs recompute exactly th
   cfg3  (10^5 instances x 64 nodes, p = 0.2, AVERAGE, eps = 1e-6): instances_digest = sha256 over
         the concatenated per-instance sha256(x_b) digests in global instance order (composable
         over any instance sharding: a checksum of checksums), and sha256 of the rounds array.
-  cfg4  (N = 2^20, the bench workload): sha256 of x after 100 FIXED rounds; cfg4_eps rounds + sha.
+  cfg4  (N = 2^20, the bench workload): sha256 of x after 100 FIXED rounds in fp64 and in fp32 mode
+        (DESIGN.md §9); cfg4_eps rounds + sha.
+
+`python tests/golden/make_golden_fullsize.py cfg4` regenerates only the named sections and keeps
+the others.
 """
 from __future__ import annotations
 
@@ -93,6 +97,10 @@ def cfg4_golden() -> dict:
     with O.OracleSimulator(cfg, threads=THREADS) as o:
         o.run()
         out["fixed100_x_sha256"] = sha256_values(o.values(0))
+    cfg = preset("cfg4", max_rounds=100, dtype="f32")
+    with O.OracleSimulator(cfg, threads=THREADS) as o:
+        o.run()
+        out["f32_fixed100_x_sha256"] = sha256_values(o.values(0))
     cfg = preset("cfg4_eps")
     with O.OracleSimulator(cfg, threads=THREADS) as o:
         o.run()
@@ -103,9 +111,13 @@ def cfg4_golden() -> dict:
 
 def main() -> None:
     O.build()
-    out = {"generator": "tests/golden/make_golden_fullsize.py (oracle/acs_oracle.c)",
-           "cfg3": cfg3_golden(), "cfg4": cfg4_golden(), "cfg5": cfg5_golden()}
     path = os.path.join(HERE, "fullsize.json")
+    makers = {"cfg3": cfg3_golden, "cfg4": cfg4_golden, "cfg5": cfg5_golden}
+    names = sys.argv[1:] or list(makers)
+    out = json.load(open(path)) if sys.argv[1:] and os.path.exists(path) else {}
+    out["generator"] = "tests/golden/make_golden_fullsize.py (oracle/acs_oracle.c)"
+    for nm in names:
+        out[nm] = makers[nm]()
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
     print("wrote", path)

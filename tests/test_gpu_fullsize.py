@@ -55,6 +55,16 @@ def test_cfg4_full_size_bit_exact(oracle_mod, name, over):
     assert np.array_equal(bits(gt), bits(ot)), "spread traces differ"
 
 
+def test_cfg4_f32_fixed100_matches_golden():
+    """fp32 mode of the bench workload (100 FIXED rounds) against the oracle-written hash that
+    bench.py's cfg4_f32 leg checks."""
+    cfg = preset("cfg4", max_rounds=100, dtype="f32", trace_spread=True)
+    kname, gr, gx, gt = run_gpu(cfg)
+    assert kname.startswith("k_bin_scatter"), kname
+    assert int(gr[0]) == 100
+    assert sha256_values(gx) == GOLDEN["cfg4"]["f32_fixed100_x_sha256"]
+
+
 def test_cfg4_full_size_properties():
     """Validity and contraction of the trimmed mean without faults: every value stays inside the
     hull of x^0, and the honest spread never grows from one round to the next."""
