@@ -329,8 +329,13 @@ constexpr uint32_t kBinPartCap = D * kBinSB / NP + D * kBinSB / 16;   // + 1/16 
 
 // VAR: a CSR graph padded to D (§8(f) row 1): slots t >= deg(i) are absent entries, slot numbers
 // are rowptr[i] + t (one drop draw each); single pass only.
+// Faulty NP > 1: the parts' LDS buffers admit 4 workgroups per CU, so ask for 4 waves per SIMD (at
+// most 128 VGPRs; unbounded the faulty instantiations take 163-179 and run 3 workgroups per CU)
+#ifndef ACS_FAULTY_WPE
+#define ACS_FAULTY_WPE 4
+#endif
 template <int D, int T, bool WMSR = false, bool FAULTY = false, typename VT = double, int NP = 1, bool VAR = false>
-__global__ __launch_bounds__(kBinSB) void k_bin_gather(const RoundArgs a, const VT* __restrict__ stage,
+__global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE : 1) void k_bin_gather(const RoundArgs a, const VT* __restrict__ stage,
                                                        const uint16_t* __restrict__ invpos,
                                                        const uint2* __restrict__ tiles, uint32_t nrun, uint32_t Q,
                                                        uint32_t Qc, uint32_t pol) {
