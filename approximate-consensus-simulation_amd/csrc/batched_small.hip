@@ -152,10 +152,13 @@ __device__ __forceinline__ VT average_tree_sel(const VT* xs, VT xi, uint64_t use
     return acc[LOG2P];
 }
 
+#ifndef ACS_BATCHED_WPE
+#define ACS_BATCHED_WPE 4   // waves per SIMD asked of the compiler (VGPR budget 512 / WPE)
+#endif
 // VT = double, or float in fp32 mode: every §A.7 step in binary32, spread =
 // binary32(hi - lo) compared as a double, lo / hi / spread kept as doubles in InstState.
 template <int P, bool SORT, bool FAULTS, typename VT = double>
-__global__ __launch_bounds__(64) void k_batched_small(const BatchArgs a, uint32_t kmax) {
+__global__ __launch_bounds__(64, (!SORT && !FAULTS) ? ACS_BATCHED_WPE : 1) void k_batched_small(const BatchArgs a, uint32_t kmax) {
     const uint32_t lb = blockIdx.x;
     const uint32_t lane = threadIdx.x;
     InstState* S = a.st + lb;
