@@ -247,3 +247,46 @@ def test_gpu_binned_exchange_random_configs(oracle_mod, case):
     assert np.array_equal(gr, o["rounds"]), (cfg, sa, name)
     assert np.array_equal(_bits(gx), _bits(o["x"][0])), (cfg, sa, name)
     assert np.array_equal(_bits(gt), _bits(o["trace"][0])), (cfg, sa, name)
+
+
+@st.composite
+def partition_cases(draw):
+    """Node-partitioned runs (SURVEY §8(e), cfg5's data flow) on virtual partitions: a binned or
+    per-lane config, 2-8 row blocks, the chunked or the all-gather exchange, small source blocks."""
+    cfg, sa = draw(binned_configs())
+    if draw(st.booleans()):   # also the per-lane kernel's partitioned path: (4, 0) / (4, 1) have
+        t = draw(st.sampled_from([0, 1]))   # compiled register variants but no binned plan
+        rule = draw(st.sampled_from(["trimmed", "midpoint", "wmsr", "dlpsw"] if t else
+                                    ["average", "trimmed", "midpoint"]))
+        cfg = cfg.replace(degree=4, trim=t, rule=rule)
+    return cfg, sa, draw(st.integers(2, 8)), draw(st.sampled_from(["0", "2", "4"]))
+
+
+@pytest.mark.gpu
+@settings(max_examples=100, deadline=None, derandomize=True, database=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+@given(case=partition_cases())
+def test_gpu_virtual_partitions_random_configs(oracle_mod, case):
+    """Every private copy of x equals the oracle's unpartitioned run, bit for bit."""
+    import os
+    import acsim
+    cfg, sa, parts, xchunks = case
+    old = {k: os.environ.get(k) for k in ("ACSIM_BIN_SA", "ACSIM_XCHUNKS")}
+    os.environ["ACSIM_BIN_SA"] = str(sa)
+    os.environ["ACSIM_XCHUNKS"] = xchunks
+    try:
+        with acsim.Simulator(cfg, partitions=parts) as p:
+            p.run()
+            pr, pt = p.rounds(), p.spread_trace(0)
+            copies = [p.partition_values(q) for q in range(parts)]
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    o = _run_oracle(oracle_mod, cfg.replace(omp_threads=16))
+    assert np.array_equal(pr, o["rounds"]), (cfg, sa, parts, xchunks)
+    assert np.array_equal(_bits(pt), _bits(o["trace"][0])), (cfg, sa, parts, xchunks)
+    for q, x in enumerate(copies):
+        assert np.array_equal(_bits(x), _bits(o["x"][0])), (cfg, sa, parts, xchunks, q)
