@@ -290,3 +290,26 @@ def test_gpu_virtual_partitions_random_configs(oracle_mod, case):
     assert np.array_equal(_bits(pt), _bits(o["trace"][0])), (cfg, sa, parts, xchunks)
     for q, x in enumerate(copies):
         assert np.array_equal(_bits(x), _bits(o["x"][0])), (cfg, sa, parts, xchunks, q)
+
+
+@pytest.mark.gpu
+@settings(max_examples=150, deadline=None, derandomize=True, database=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+@given(cfg=configs(max_n=300), frac=st.floats(0.0, 1.0))
+def test_gpu_resume_random_configs(oracle_mod, cfg, frac):
+    """Checkpoint / resume: rounds stopped at r0, the values read back and set into a
+    fresh handle with acs_set_state(r0, x^r0), then run to the end, equal the oracle's straight
+    run bit for bit (synchronous rounds: with delays set_state restarts the history by design)."""
+    import acsim
+    cfg = cfg.replace(delay_max=0)
+    o = _run_oracle(oracle_mod, cfg)
+    r0 = int(frac * int(o["rounds"].min()))
+    with acsim.Simulator(cfg, device=0) as a:
+        a.round(r0)
+        xr = a.all_values()
+    with acsim.Simulator(cfg, device=0) as b:
+        b.set_state(r0, xr)
+        b.run()
+        br, bx = b.rounds(), b.all_values()
+    assert np.array_equal(br, o["rounds"]), (cfg, r0)
+    assert np.array_equal(_bits(bx), _bits(o["x"])), (cfg, r0)
