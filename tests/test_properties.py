@@ -313,3 +313,52 @@ def test_gpu_resume_random_configs(oracle_mod, cfg, frac):
         br, bx = b.rounds(), b.all_values()
     assert np.array_equal(br, o["rounds"]), (cfg, r0)
     assert np.array_equal(_bits(bx), _bits(o["x"])), (cfg, r0)
+
+
+@pytest.mark.gpu
+@settings(max_examples=100, deadline=None, derandomize=True, database=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+@given(cfg=configs(max_n=300), steps=st.lists(st.integers(1, 17), min_size=1, max_size=6))
+def test_gpu_round_steps_equal_run(cfg, steps):
+    """Simulator.round(k) in arbitrary steps (the chunked enqueue loop, EPS polling, deferred
+    finalize across calls) ends exactly where one run() does."""
+    import acsim
+    with acsim.Simulator(cfg, device=0) as a:
+        a.run()
+        ar, ax = a.rounds(), a.all_values()
+        at = [a.spread_trace(b) for b in range(cfg.n_instances)]
+    with acsim.Simulator(cfg, device=0) as b:
+        k = 0
+        while True:
+            info = b.round(steps[k % len(steps)])
+            k += 1
+            if info.done or k > 10_000:
+                break
+        br, bx = b.rounds(), b.all_values()
+        bt = [b.spread_trace(i) for i in range(cfg.n_instances)]
+    assert np.array_equal(br, ar), (cfg, steps)
+    assert np.array_equal(_bits(bx), _bits(ax)), (cfg, steps)
+    for i in range(cfg.n_instances):
+        assert np.array_equal(_bits(bt[i]), _bits(at[i])), (cfg, steps, i)
+
+
+@pytest.mark.gpu
+@settings(max_examples=60, deadline=None, derandomize=True, database=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+@given(cfg=configs(max_n=200), cut=st.integers(1, 7))
+def test_gpu_instance_shards_equal_batch(cfg, cut):
+    """instances are seeded by their global id, so any split of a batch into
+    instance_offset windows (one per rank) reproduces the batch exactly."""
+    import acsim
+    B = 8
+    cfg = cfg.replace(n_instances=B)
+    with acsim.Simulator(cfg, device=0) as a:
+        a.run()
+        ar, ax = a.rounds(), a.all_values()
+    parts = [(0, cut), (cut, B - cut)]
+    for off, cnt in parts:
+        sub = cfg.replace(n_instances=cnt, instance_offset=int(cfg.instance_offset) + off)
+        with acsim.Simulator(sub, device=0) as s:
+            s.run()
+            assert np.array_equal(s.rounds(), ar[off:off + cnt]), (cfg, cut)
+            assert np.array_equal(_bits(s.all_values()), _bits(ax[off:off + cnt])), (cfg, cut)
