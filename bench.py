@@ -117,15 +117,31 @@ def lib_sha256() -> str:
         return hashlib.sha256(f.read()).hexdigest()
 
 
+def src_sha256() -> str:
+    """sha256 over the HIP library's sources (csrc/*.hip, *.hpp, the Makefile, include/acsim.h):
+    a rebuild of unchanged sources keeps it, while the library's own hash may change (the
+    toolchain's output is not byte-reproducible across build directories)."""
+    csrc = os.path.join(PKG, "csrc")
+    files = sorted(f for f in os.listdir(csrc) if f.endswith((".hip", ".hpp")) or f == "Makefile")
+    h = hashlib.sha256()
+    for f in files + ["../../include/acsim.h"]:
+        with open(os.path.join(csrc, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()
+
+
 def load_pmc(kernel: str, n_nodes: int, dtype: str = "f64"):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if it was taken on this
-    exact build of libacsim.so (same kernel name, size and library sha256); else None."""
+    build of libacsim.so — same kernel name and size, and the same library sha256 or the same
+    sha256 of the kernel sources — else None."""
     path = os.path.join(ROOT, "profiles", "pmc_cfg4.json" if dtype == "f64" else "pmc_cfg4_f32.json")
     try:
         d = json.load(open(path))
     except Exception:
         return None
-    if d.get("kernel") == kernel and d.get("n_nodes") == n_nodes and d.get("lib_sha256") == lib_sha256():
+    if d.get("kernel") != kernel or d.get("n_nodes") != n_nodes:
+        return None
+    if d.get("lib_sha256") == lib_sha256() or d.get("src_sha256") == src_sha256():
         return d.get("hbm_bytes_per_launch")
     return None
 
