@@ -18,7 +18,8 @@ standalone k_finalize per 16-round chunk is not.  Every --event-every-th timed r
 is bracketed: an event pair idles the stream for ~5 µs, which would otherwise inflate ms_per_step.
 `traffic` is the pair's measured HBM bytes per round from the committed rocprofv3 PMC summary
 (profiles/pmc_cfg4.json, FETCH_SIZE x 2 + WRITE_SIZE, tools/traffic_json.py); it is reported only
-when that summary was taken on this exact libacsim.so (sha256 match), else null.
+when that summary was taken on this build (same library sha256, or the same sha256 of the kernel
+sources: a rebuild of unchanged sources is not byte-identical), else null.
 cpu_baseline times the CPU oracle (this repo's spec restatement, oracle/) on rank 0 on a bounded
 sample of the same workload.
 
