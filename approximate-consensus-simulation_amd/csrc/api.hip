@@ -914,6 +914,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     // order-free phase B (clean, sort-based rule: the rows are stored sorted and the rule sees a
     // multiset), ACSIM_BIN_OF=1: measured slower than the invpos phase B, kept as
     // a tested variant
+    std::string kname_lane;   // (set with the binned decision below)
     const char* of_env = getenv("ACSIM_BIN_OF");
     // (rid is one byte per entry: receiver blocks of at most 256)
     const bool bin_of = s->ell_sorted && of_env && of_env[0] == '1' && !s->csr_var && kBinSB <= 256;
@@ -931,6 +932,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
                     binned_supported(s->d, cfg->trim, cfg->rule) && rows_local * s->d < (1ull << 32);
         const char* df = getenv("ACSIM_DEFER_FIN");
         s->defer_fin = s->binned && !partitioned && s->B == 1 && !(df && df[0] == '0');
+        kname_lane = s->kname;   // the per-lane kernel's name, should a binned plan not fit (below)
         if (s->binned) {
             char nm[96];
             snprintf(nm, sizeof nm, "k_bin_scatter+%sk_bin_gather<%u,%u%s%s>%s", lv == 2 ? "k_bin_regroup+" : "", s->d,
@@ -995,15 +997,21 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         CREATE_TRY(hipMalloc(&s->ell, words * sizeof(uint32_t)));
         CREATE_TRY(hipMemsetAsync(s->ell, 0, words * sizeof(uint32_t), s->stream));
         CREATE_TRY(build_rows(s, s->ell, partitioned ? rank : 0));
-        if (s->binned) {   // the plan replaces the ELL in the round loop
-            const uint64_t nr = partitioned ? part_rows(s, rank) : s->N;
-            if (nr) CREATE_TRY(binned_build(s->bin, s->ell, s->N, nr, s->d, s->dp, bin_sa, tagged, s->f32, bin_of, s->stream));
-            // NP-pass phase B (slot-dependent configs: fp64, two passes only; see launch_round_binned)
-            if (s->bin.split > 1 && (s->clean || (!s->f32 && s->bin.split == 2)))
-                s->kname += " split" + std::to_string(s->bin.split);
-            (void)hipFree(s->ell);
-            s->ell = nullptr;
-        }
+        // The binned plans replace the ELLs in the round loop.  A plan can still be refused after
+        // it is laid out (a two-level plan whose phase-M image outgrows the LDS, too many runs
+        // per receiver block): then every partition keeps its ELL and runs the per-lane kernel,
+        // which serves the same configs (binned_supported implies a compiled register variant).
+        bool bin_refused = false;
+        auto try_plan = [&](BinnedPlan& plan, const uint32_t* ell, uint64_t nr) -> hipError_t {
+            if (!s->binned || bin_refused || !nr) return hipSuccess;
+            hipError_t e = binned_build(plan, ell, s->N, nr, s->d, s->dp, bin_sa, tagged, s->f32, bin_of, s->stream);
+            if (e == hipErrorNotSupported) {
+                bin_refused = true;
+                return hipSuccess;
+            }
+            return e;
+        };
+        CREATE_TRY(try_plan(s->bin, s->ell, partitioned ? part_rows(s, rank) : s->N));
         if (virt) {
             s->parts.resize(nranks - 1);
             for (int p = 1; p < nranks; ++p) {
@@ -1013,12 +1021,25 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
                 CREATE_TRY(hipMalloc(&q.ell, words * sizeof(uint32_t)));
                 CREATE_TRY(hipMemsetAsync(q.ell, 0, words * sizeof(uint32_t), s->stream));
                 CREATE_TRY(build_rows(s, q.ell, p));
-                if (s->binned) {
-                    const uint64_t nr = part_rows(s, p);
-                    if (nr) CREATE_TRY(binned_build(q.bin, q.ell, s->N, nr, s->d, s->dp, bin_sa, tagged, s->f32, bin_of, s->stream));
-                    (void)hipFree(q.ell);
-                    q.ell = nullptr;
-                }
+                CREATE_TRY(try_plan(q.bin, q.ell, part_rows(s, p)));
+            }
+        }
+        if (s->binned && bin_refused) {
+            binned_free(s->bin);
+            for (Part& q : s->parts) binned_free(q.bin);
+            s->binned = false;
+            s->defer_fin = false;
+            s->kname = kname_lane + (s->f32 ? " [f32]" : "");
+        }
+        if (s->binned) {
+            // NP-pass phase B (slot-dependent configs: fp64, two passes only; see launch_round_binned)
+            if (s->bin.split > 1 && (s->clean || (!s->f32 && s->bin.split == 2)))
+                s->kname += " split" + std::to_string(s->bin.split);
+            (void)hipFree(s->ell);
+            s->ell = nullptr;
+            for (Part& q : s->parts) {
+                (void)hipFree(q.ell);
+                q.ell = nullptr;
             }
         }
     }
@@ -1062,10 +1083,18 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
             CREATE_TRY(launch_csr_to_ell(s->rowptr, s->colidx, s->N, s->d, s->ell, s->deg, s->sw, s->stream));
             if (s->ell_sorted) CREATE_TRY(launch_sort_ell_rows(s->ell, s->N, s->d, s->stream));
             if (s->binned) {
-                CREATE_TRY(binned_build(s->bin, s->ell, s->N, s->N, s->d, s->dp, bin_sa, tagged, s->f32, false, s->stream,
-                                        true));
-                (void)hipFree(s->ell);
-                s->ell = nullptr;
+                const hipError_t be = binned_build(s->bin, s->ell, s->N, s->N, s->d, s->dp, bin_sa, tagged, s->f32, false,
+                                                   s->stream, true);
+                if (be == hipErrorNotSupported) {   // the plan does not fit: the per-lane kernel serves the rows
+                    binned_free(s->bin);
+                    s->binned = false;
+                    s->defer_fin = false;
+                    s->kname = kname_lane + (s->n_hub ? "+k_round_generic(hubs)" : "") + (s->f32 ? " [f32]" : "");
+                } else {
+                    CREATE_TRY(be);
+                    (void)hipFree(s->ell);
+                    s->ell = nullptr;
+                }
             }
         }
     }

@@ -139,3 +139,33 @@ def test_chunked_exchange_single_rank_rccl():
             p.run()
             assert np.array_equal(bits(p.values(0)), bits(ref.values(0)))
             assert np.array_equal(bits(p.spread_trace(0)), bits(ref.spread_trace(0)))
+
+
+def test_refused_binned_plan_falls_back_to_per_lane(oracle_mod):
+    """A partition whose binned plan is refused once laid out (found by tools/fuzz_gpu.py: 46 081
+    nodes, 8-regular, source blocks of 256, 3 partitions — a two-level plan whose phase-M image
+    outgrows the LDS) must not fail acs_create: every partition runs the per-lane kernel instead,
+    bit-exact against the oracle."""
+    import os
+    cfg = Config(n_nodes=46081, topology="regular", degree=8, rule="average", eps=1e-7, max_rounds=20,
+                 seed=3, trace_spread=True)
+    old = os.environ.get("ACSIM_BIN_SA")
+    os.environ["ACSIM_BIN_SA"] = "256"
+    try:
+        with acsim.Simulator(cfg, partitions=3) as p:
+            name = p.kernel_name()
+            p.run()
+            pr, px = p.rounds(), p.values(0)
+            copies = [p.partition_values(q) for q in range(3)]
+    finally:
+        if old is None:
+            os.environ.pop("ACSIM_BIN_SA", None)
+        else:
+            os.environ["ACSIM_BIN_SA"] = old
+    assert name.startswith("k_round_regular"), name
+    with oracle_mod.OracleSimulator(cfg, threads=8) as o:
+        o.run()
+        assert np.array_equal(pr, o.rounds())
+        assert np.array_equal(bits(px), bits(o.values(0)))
+        for x in copies:
+            assert np.array_equal(bits(x), bits(o.values(0)))
