@@ -29,7 +29,9 @@ def configs(draw, max_n=160):
     """A valid small Config (acs_create's admission rules, include/acsim.h)."""
     topo = draw(st.sampled_from(["complete", "random_regular"]))
     if topo == "complete":
-        n = draw(st.integers(3, 40))
+        # batched (N <= 64), dense persistent (Byzantine SPLIT / CONSTANT or clean) and generic
+        # (loss / crash / RANDOM above 64 nodes) kernels
+        n = draw(st.one_of(st.integers(3, 40), st.integers(41, 300)))
         d = 0
         m = n
     else:
@@ -75,7 +77,7 @@ def csr_configs(draw, max_n=300):
     """A user graph (ACS_TOPO_CSR, §8(f) row 1) with random degrees and senders, and a valid
     Config for it: (cfg, (rowptr, colidx))."""
     n = draw(st.integers(8, max_n))
-    dmin = draw(st.integers(1, 12))
+    dmin = draw(st.integers(0, 12))   # 0: rows without senders (m_i = 1)
     dmax = dmin + draw(st.sampled_from([0, 3, 20, 60]))
     rng = np.random.default_rng(draw(st.integers(0, 2 ** 32)))
     deg = rng.integers(dmin, dmax + 1, size=n)
