@@ -1,5 +1,5 @@
 """Long randomized GPU-vs-oracle sweep (the strategies of tests/test_properties.py, not
-derandomized): python tools/fuzz_gpu.py [--examples 2000] [--seed S] [--which configs,csr,binned,partitions,resume,steps]
+derandomized): python tools/fuzz_gpu.py [--examples 2000] [--seed S] [--which configs,csr,binned,partitions,resume,steps,hubs]
 
 Prints one line per strategy with the number of passing draws, or the falsifying example.
 """
@@ -38,6 +38,32 @@ def main():
     }
     for name, (fn, args) in multi.items():
         tests[name] = (fn, args, None)
+
+    # CSR graphs with hub rows (fast path + generic size classes + the big-m path above 8192
+    # entries): a few heavy draws, checked like test_gpu_matches_oracle_random_csr
+    import numpy as np
+
+    @st.composite
+    def hub_cases(draw):
+        n = draw(st.integers(9000, 20000))
+        rng = np.random.default_rng(draw(st.integers(0, 2 ** 32)))
+        deg = rng.integers(draw(st.integers(3, 11)), 33, size=n)
+        nh = draw(st.integers(1, 6))
+        hubs = rng.choice(n, size=nh, replace=False)
+        deg[hubs] = rng.integers(40, 12000, size=nh)
+        rowptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.uint64)
+        colidx = rng.integers(0, n, size=int(rowptr[-1])).astype(np.uint32)
+        base = draw(T.configs())
+        tmax = int(deg.min()) // 2
+        rule = base.rule
+        t = 0 if rule == "average" else draw(st.integers(1 if rule == "dlpsw" else 0, max(tmax, 1)))
+        if t > tmax:
+            rule, t = "average", 0
+        cfg = base.replace(topology="csr", n_nodes=n, degree=0, rule=rule, trim=t, n_instances=1,
+                           n_faulty=min(base.n_faulty, n // 10), max_rounds=min(base.max_rounds, 12))
+        return cfg, (rowptr, colidx)
+
+    tests["hubs"] = (T.test_gpu_matches_oracle_random_csr, "case", hub_cases())
     for name in a.which.split(","):
         if name not in tests:
             continue
