@@ -15,6 +15,7 @@
 // O(N^2 log^2 N) work per round.  Rounds in which a crash sender delivers partially (r == r_v),
 // message loss, AVERAGE and RANDOM Byzantine values keep the generic kernel.
 #include <mutex>
+#include <type_traits>
 #include "resolve.hpp"
 
 namespace acs {
@@ -177,10 +178,38 @@ struct Merged {   // M = B with two constant blocks (v1 <= v2) spliced in at the
 template <typename VT = double>
 struct Runs3 {
     using value_type = VT;
-    VT v[3];
-    uint32_t e[2];
-    __device__ __forceinline__ VT at(uint32_t k) const { return k < e[0] ? v[0] : k < e[1] ? v[1] : v[2]; }
+    VT v0, v1, v2;
+    uint32_t e0, e1;
+    // A bitwise blend of all three values, not a select of two loads: the compiler folds the
+    // latter into a load through a selected address, which pins the struct in scratch memory.
+    __device__ __forceinline__ VT at(uint32_t k) const {
+        using U = __UINT64_TYPE__;
+        using B = typename std::conditional<sizeof(VT) == 8, U, uint32_t>::type;
+        const B m0 = (B)0 - (B)(k < e0), m1 = (B)0 - (B)(k < e1);
+        const B b0 = __builtin_bit_cast(B, v0), b1 = __builtin_bit_cast(B, v1), b2 = __builtin_bit_cast(B, v2);
+        return __builtin_bit_cast(VT, (b0 & m0) | (~m0 & ((b1 & m1) | (~m1 & b2))));
+    }
 };
+
+// Lane l receives lane l + O's 32-bit value (O = 32, 16: v_permlane32_swap / v_permlane16_swap,
+// whose second result carries the upper half / odd rows into the lower half / even rows; O <= 8:
+// DPP row_shl within a 16-lane row).  Only the lanes l < O are meaningful.
+template <int O>
+__device__ __forceinline__ uint32_t lane_up_u32(uint32_t x) {
+    if constexpr (O == 32) return __builtin_amdgcn_permlane32_swap(x, x, false, false)[1];
+    else if constexpr (O == 16) return __builtin_amdgcn_permlane16_swap(x, x, false, false)[1];
+    else return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x100 + O, 0xF, 0xF, false);
+}
+template <int O>
+__device__ __forceinline__ double lane_up(double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint64_t lo = lane_up_u32<O>((uint32_t)b), hi = lane_up_u32<O>((uint32_t)(b >> 32));
+    return __builtin_bit_cast(double, lo | (hi << 32));
+}
+template <int O>
+__device__ __forceinline__ float lane_up(float v) {
+    return __builtin_bit_cast(float, lane_up_u32<O>(__builtin_bit_cast(uint32_t, v)));
+}
 
 // The rule over the window R = M[t, m - t) of one receiver's merged sorted sequence, by one
 // wavefront (§A.7 stride-halving tree sum spread over the 64 lanes); every lane returns the result.
@@ -224,12 +253,16 @@ __device__ __forceinline__ VT dense_window(const Seq& M, uint32_t rule, uint32_t
                 for (uint32_t g = 0; g < s; ++g) col[g] = col[g] + col[g + s];
             w[0] = col[0];
         }
+        // strides 32 .. 1 across lanes: lane l < o adds lane l + o (lanes >= o compute values
+        // nobody reads).  Register-to-register moves instead of LDS permutes: the gfx950 permlane
+        // swaps for 32 and 16, DPP row shifts within a 16-lane row for 8 .. 1.
         VT v = w[0];
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            const VT u = __shfl_down(v, o, 64);
-            if (lane < (uint32_t)o) v = v + u;
-        }
+        v = v + lane_up<32>(v);
+        v = v + lane_up<16>(v);
+        v = v + lane_up<8>(v);
+        v = v + lane_up<4>(v);
+        v = v + lane_up<2>(v);
+        v = v + lane_up<1>(v);
         res = readlane_v(v, 0) / (VT)cnt;
     }
     return res;
@@ -341,36 +374,34 @@ __global__ __launch_bounds__(kDenseSortBlock) void k_dense_persist(const BatchAr
     }
     const uint32_t nzv = cnt[1], nbv = N - nzv;
     const uint32_t ncls = (nzv && mp.byz == 0) ? 2u : 1u;   // SPLIT: parity classes
-    const uint32_t ncnt[2] = {ncls == 2 ? cnt[2] : nbv, ncls == 2 ? cnt[3] : 0u};
+    // (scalars, not arrays: a runtime-indexed array lands in scratch, and the per-round class loop
+    // then waited on two dependent scratch round trips per class)
+    const uint32_t ncnt0 = ncls == 2 ? cnt[2] : nbv, ncnt1 = ncls == 2 ? cnt[3] : 0u;
     // After any round every non-Byzantine node holds its class's value (its multiset is the base,
     // which contains its own entry, plus its class's Byzantine block), and in these configs every
     // non-Byzantine node is honest (dense_supported admits no crash schedules).  So after the first
     // round of a launch (the base sort) a round is ≤ 2 window rules on three constant runs, one
     // wave per class, and the honest (min, max) is the (min, max) of the populated classes: one
     // barrier per round, and x is written out once at the end.  (Wave 0 alone evaluating both
-    // windows without a barrier measured slower: cfg2 2.25 against 2.0 ms.)
-    bool classed = false;   // cl[] holds every non-Byzantine node's value
-    VT cl[2] = {VT(0), VT(0)};
-    auto window_classed = [&](uint32_t wc) -> VT {   // base = {cl0 x n0, cl1 x n1} + {c x nz}
+    // windows without a barrier measured slower: cfg2 2.25 against 2.0 ms, and again 1.35 against
+    // 0.98 ms once the class values stayed in registers and the tree used permlane / DPP moves.)
+    bool classed = false;   // cl0 / cl1 hold every non-Byzantine node's value
+    VT cl0 = VT(0), cl1 = VT(0);
+    // (the class values come in as arguments, not by reference: a select between two referenced
+    // locals also becomes a load through a selected address)
+    auto window_classed = [&](uint32_t wc, VT cl0, VT cl1) -> VT {   // base = {cl0 x n0, cl1 x n1} + {c x nz}
         const VT c = dense_byz(mp, wc, lo, hi, VT(0));
-        VT bv[2] = {cl[0], cl[1]};
-        uint32_t bn[2] = {ncnt[0], ncnt[1]};
-        if (ncls == 2 && bv[1] < bv[0]) {
-            const VT tv = bv[0]; bv[0] = bv[1]; bv[1] = tv;
-            const uint32_t tn = bn[0]; bn[0] = bn[1]; bn[1] = tn;
-        }
+        const bool sw = ncls == 2 && cl1 < cl0;   // base runs in value order
+        const VT b0 = sw ? cl1 : cl0, b1 = sw ? cl0 : cl1;
+        const uint32_t n0 = sw ? ncnt1 : ncnt0, n1 = sw ? ncnt0 : ncnt1;
         // insert the Byzantine block before the first base run with a value >= c
+        const uint32_t pos = (nzv == 0 || c <= b0) ? 0u : (ncls == 1 || c <= b1) ? 1u : 2u;
         Runs3<VT> R;
-        if (nzv == 0 || c <= bv[0]) {
-            R.v[0] = c; R.v[1] = bv[0]; R.v[2] = bv[1];
-            R.e[0] = nzv; R.e[1] = nzv + bn[0];
-        } else if (ncls == 1 || c <= bv[1]) {
-            R.v[0] = bv[0]; R.v[1] = c; R.v[2] = bv[1];
-            R.e[0] = bn[0]; R.e[1] = bn[0] + nzv;
-        } else {
-            R.v[0] = bv[0]; R.v[1] = bv[1]; R.v[2] = c;
-            R.e[0] = bn[0]; R.e[1] = bn[0] + bn[1];
-        }
+        R.v0 = pos == 0 ? c : b0;
+        R.v1 = pos == 0 ? b0 : pos == 1 ? c : b1;
+        R.v2 = pos == 2 ? c : b1;
+        R.e0 = pos == 0 ? nzv : n0;
+        R.e1 = pos == 0 ? nzv + n0 : pos == 1 ? n0 + nzv : n0 + n1;
         return dense_window(R, a.rule, N, a.trim, lane);
     };
     for (uint32_t q = 0; q < kmax && !done; ++q) {
@@ -401,20 +432,23 @@ __global__ __launch_bounds__(kDenseSortBlock) void k_dense_persist(const BatchAr
                 if (lane == 0) cls[q & 1u][w] = res;
             }
         } else if (w < ncls) {
-            const VT res = window_classed(w);
+            const VT res = window_classed(w, cl0, cl1);
             if (lane == 0) cls[q & 1u][w] = res;
         }
         __syncthreads();   // (round q + 1 writes the other buffer; round q + 2 writes this one
                            // only after every wave has passed round q + 1's barrier)
-        cl[0] = cls[q & 1u][0];
-        cl[1] = ncls == 2 ? cls[q & 1u][1] : cl[0];
+        cl0 = cls[q & 1u][0];
+        cl1 = ncls == 2 ? cls[q & 1u][1] : cl0;
         classed = true;
         double mn = kInf, mx = -kInf;
-        for (uint32_t c = 0; c < ncls; ++c)
-            if (ncnt[c]) {   // classes with members
-                mn = __builtin_fmin(mn, (double)cl[c]);
-                mx = __builtin_fmax(mx, (double)cl[c]);
-            }
+        if (ncnt0) {   // classes with members
+            mn = __builtin_fmin(mn, (double)cl0);
+            mx = __builtin_fmax(mx, (double)cl0);
+        }
+        if (ncls == 2 && ncnt1) {
+            mn = __builtin_fmin(mn, (double)cl1);
+            mx = __builtin_fmax(mx, (double)cl1);
+        }
         r += 1;
         lo = mn;
         hi = mx;
@@ -425,7 +459,7 @@ __global__ __launch_bounds__(kDenseSortBlock) void k_dense_persist(const BatchAr
     }
     VT* xout = reinterpret_cast<VT*>((r & 1u) ? a.x1 : a.x0) + (uint64_t)lb * N;
     for (uint32_t j = tid; j < N; j += kDenseSortBlock)
-        xout[j] = (classed && !byz[j]) ? cl[ncls == 2 ? (j & 1u) : 0u] : xs[j];
+        xout[j] = (classed && !byz[j]) ? ((ncls == 2 && (j & 1u)) ? cl1 : cl0) : xs[j];
     if (tid == 0) {
         S->lo = lo;
         S->hi = hi;
