@@ -223,6 +223,47 @@ def binned_configs(draw):
     return cfg, draw(st.sampled_from([256, 512, 1024, 4096]))
 
 
+@st.composite
+def dense_configs(draw, max_n=600):
+    """Complete graphs the persistent dense kernel serves (round_dense.hip: 65 .. 4096 nodes, clean
+    or Byzantine SPLIT / CONSTANT, no loss, no crash, no delays; the sort-based rules): windows of
+    64 .. 512 slots, one or two Byzantine classes, fp64 and fp32."""
+    base = draw(configs())
+    n = draw(st.integers(65, max_n))
+    rule = draw(st.sampled_from(["trimmed", "midpoint", "dlpsw"]))   # (AVERAGE / W-MSR: other kernels)
+    tmax = (n - 1) // 2
+    t = draw(st.integers(1 if rule == "dlpsw" else 0, tmax))
+    fault = draw(st.sampled_from(["none", "byzantine", "byzantine"]))
+    kw = dict(fault_model=fault, n_faulty=0)
+    if fault == "byzantine":
+        kw.update(n_faulty=draw(st.integers(1, max(1, n // 3))),
+                  byz_strategy=draw(st.sampled_from(["split", "constant"])))
+    return base.replace(topology="complete", n_nodes=n, degree=0, rule=rule, trim=t, loss_p=0.0,
+                        delay_max=0, missing_policy="self", n_instances=draw(st.integers(1, 2)),
+                        max_rounds=min(base.max_rounds, 40), **kw)
+
+
+@pytest.mark.gpu
+@settings(max_examples=60, deadline=None, derandomize=True, database=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+@given(cfg=dense_configs())
+def test_gpu_dense_random_configs(oracle_mod, cfg):
+    """The persistent dense kernel (one workgroup per instance, class windows with permlane / DPP
+    tree sums) against the oracle."""
+    import acsim
+    with acsim.Simulator(cfg, device=0) as g:
+        name = g.kernel_name()
+        g.run()
+        gr, gx = g.rounds(), g.all_values()
+        gt = [g.spread_trace(b) for b in range(cfg.n_instances)]
+    assert "k_dense_persist" in name, (cfg, name)   # the draw must land on the dense kernel
+    o = _run_oracle(oracle_mod, cfg.replace(omp_threads=16))
+    assert np.array_equal(gr, o["rounds"]), (cfg, name)
+    assert np.array_equal(_bits(gx), _bits(o["x"])), (cfg, name)
+    for b in range(cfg.n_instances):
+        assert np.array_equal(_bits(gt[b]), _bits(o["trace"][b])), (cfg, b)
+
+
 @pytest.mark.gpu
 @settings(max_examples=120, deadline=None, derandomize=True, database=None,
           suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])

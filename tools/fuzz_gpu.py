@@ -65,25 +65,8 @@ def main():
 
     tests["hubs"] = (T.test_gpu_matches_oracle_random_csr, "case", hub_cases())
 
-    # complete graphs the persistent dense kernel serves (65..4096 nodes, clean or Byzantine
-    # SPLIT / CONSTANT, no loss, no crash, no delays): window sizes from 64 to 4096 slots
-    @st.composite
-    def dense_cases(draw):
-        base = draw(T.configs())
-        n = draw(st.one_of(st.integers(65, 600), st.integers(65, 600), st.integers(601, 2048)))
-        rule = draw(st.sampled_from(["average", "trimmed", "midpoint", "dlpsw", "wmsr"]))
-        tmax = (n - 1) // 2
-        t = 0 if rule == "average" else draw(st.integers(1 if rule == "dlpsw" else 0, tmax))
-        fault = draw(st.sampled_from(["none", "byzantine", "byzantine"]))
-        kw = dict(fault_model=fault, n_faulty=0)
-        if fault == "byzantine":
-            kw.update(n_faulty=draw(st.integers(1, max(1, min(t, n // 3)) if t else max(1, n // 4))),
-                      byz_strategy=draw(st.sampled_from(["split", "constant"])))
-        return base.replace(topology="complete", n_nodes=n, degree=0, rule=rule, trim=t, loss_p=0.0,
-                            delay_max=0, missing_policy="self", n_instances=draw(st.integers(1, 2)),
-                            max_rounds=min(base.max_rounds, 40 if n <= 600 else 6), **kw)
-
-    tests["dense"] = (T.test_gpu_matches_oracle_random_configs, "cfg", dense_cases())
+    # complete graphs the persistent dense kernel serves (asserts the kernel; up to 2048 nodes)
+    tests["dense"] = (T.test_gpu_dense_random_configs, "cfg", T.dense_configs(max_n=2048))
     for name in a.which.split(","):
         if name not in tests:
             continue
