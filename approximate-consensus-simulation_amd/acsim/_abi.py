@@ -129,6 +129,8 @@ def _declare(lib: C.CDLL) -> None:
         "acs_set_kernel_timing": (i32, [vp, i32]),
         "acs_get_kernel_timing": (i32, [vp, P(C.c_double), P(u64), C.c_char_p, u64]),
         "acs_sync": (i32, [vp]),
+        "acs_device_count": (i32, []),
+        "acs_runtime_info": (i32, [C.c_char_p, u64]),
         "acs_destroy": (None, [vp]),
         "acs_last_error": (C.c_char_p, []),
         "acs_abi_version": (i32, []),
@@ -161,6 +163,31 @@ def load_library() -> C.CDLL:
         raise ImportError(f"libacsim ABI version {v} != expected {ABI_VERSION}")
     _lib = lib
     return lib
+
+
+def device_count() -> int:
+    lib = load_library()
+    n = lib.acs_device_count()
+    if n < 0:
+        check(lib, n)
+    return n
+
+
+def runtime_info() -> dict:
+    """The HIP runtime / RCCL versions libacsim.so runs on, and the files this process mapped for
+    them (/proc/self/maps): what a multi-rank run compares against the single-GPU run."""
+    lib = load_library()
+    buf = C.create_string_buffer(128)
+    check(lib, lib.acs_runtime_info(buf, 128))
+    out = {"versions": buf.value.decode()}
+    try:
+        with open("/proc/self/maps") as f:
+            paths = sorted({ln.split()[-1] for ln in f if ln.rstrip().endswith(".so") or ".so." in ln})
+    except OSError:
+        paths = []
+    for key, stem in (("libamdhip64", "libamdhip64.so"), ("librccl", "librccl.so")):
+        out[key] = [p for p in paths if os.path.basename(p).startswith(stem)]
+    return out
 
 
 def check(lib, code: int) -> None:

@@ -4,7 +4,10 @@ Independent instances (cfg3) shard with NO data-path collective: rank r owns the
 global instance block [offset, offset + count) and runs it on its own GPU; Philox counters carry
 the GLOBAL instance id (acs_config.instance_offset), so results are identical at any world size.
 The only cross-rank step is the final statistics reduction (one all_reduce of a few scalars and
-a rounds histogram), done here with torch.distributed (gloo or nccl=RCCL).
+a rounds histogram).  Every control-plane function takes `group`: an `acsim.rendezvous.Group`
+(torch-free sockets: the rank then maps only the HIP runtime and RCCL libacsim.so was built
+against; bench.py uses it) or, when `group` is None or a torch ProcessGroup, torch.distributed
+(gloo or nccl=RCCL) for callers that already run one.
 
 Single-instance configs (cfg1, cfg2, cfg4) do not shard: at N GPUs they run N independent
 replicas (distinct global instance ids), which is what bench.py measures for N > 1.
@@ -48,8 +51,22 @@ def local_stats(cfg: Config, rounds: np.ndarray, converged: np.ndarray, spread: 
                       spread_max=float(spread.max()) if spread.size else float("-inf"))
 
 
+def _is_rdzv(group) -> bool:
+    from .rendezvous import Group
+    return isinstance(group, Group)
+
+
 def reduce_stats(s: ShardStats, group=None) -> ShardStats:
-    """All-reduce shard statistics over torch.distributed (sum counts / max extrema)."""
+    """All-reduce shard statistics (sum counts / max extrema) over `group`."""
+    if _is_rdzv(group):
+        parts = group.all_gather([s.n_instances, s.n_converged, s.node_rounds, s.rounds_max,
+                                  s.rounds_hist.astype(np.int64).tobytes(), s.spread_max])
+        hist = np.zeros_like(s.rounds_hist, dtype=np.int64)
+        for p in parts:
+            hist += np.frombuffer(p[4], dtype=np.int64)
+        return ShardStats(n_instances=sum(p[0] for p in parts), n_converged=sum(p[1] for p in parts),
+                          node_rounds=sum(p[2] for p in parts), rounds_max=max(p[3] for p in parts),
+                          rounds_hist=hist, spread_max=max(p[5] for p in parts))
     import torch
     import torch.distributed as dist
     ints = torch.tensor([s.n_instances, s.n_converged, s.node_rounds], dtype=torch.int64)
@@ -63,6 +80,8 @@ def reduce_stats(s: ShardStats, group=None) -> ShardStats:
 
 
 def max_over_ranks(value: float, group=None) -> float:
+    if _is_rdzv(group):
+        return group.max(value)
     import torch
     import torch.distributed as dist
     t = torch.tensor([float(value)], dtype=torch.float64)
@@ -71,8 +90,8 @@ def max_over_ranks(value: float, group=None) -> float:
 
 
 def make_comm_id(rank: int, group=None, src: int = 0) -> bytes:
-    """RCCL unique id created on `src` and broadcast over torch.distributed (gloo or nccl)."""
-    import torch.distributed as dist
+    """RCCL unique id created on `src` and broadcast over `group` (a rendezvous Group, or
+    torch.distributed gloo / nccl)."""
     from . import _abi
     import ctypes as C
     obj = [None]
@@ -82,6 +101,9 @@ def make_comm_id(rank: int, group=None, src: int = 0) -> bytes:
         buf = C.create_string_buffer(n)
         _abi.check(lib, lib.acs_get_comm_id(buf, n))
         obj = [buf.raw]
+    if _is_rdzv(group):
+        return group.broadcast(obj[0], src=src)
+    import torch.distributed as dist
     dist.broadcast_object_list(obj, src=src, group=group)
     return obj[0]
 

@@ -928,6 +928,10 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
                                  cfg->n_faulty <= (1u << 20);
         s->binned = allow && f32_tags_ok && s->path == PATH_REGULAR && cfg->delay_max == 0 &&
                     !(s->csr_var && s->f32) &&
+                    // CSR hub rows own the partial slots after the fast path's kRegularBlock-row
+                    // blocks, and phase B writes slot b for its kBinSB-row block b: the two block
+                    // sizes must agree (an ACS_BIN_SB variant build keeps hub graphs per-lane)
+                    !(s->n_hub && kBinSB != kRegularBlock) &&
                     s->B == 1 && lv != 0 &&
                     binned_supported(s->d, cfg->trim, cfg->rule) && rows_local * s->d < (1ull << 32);
         const char* df = getenv("ACSIM_DEFER_FIN");
@@ -1146,11 +1150,17 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         CREATE_TRY(launch_init_values(q.x[0], s->B, s->N, s->mp.key, cfg->instance_offset, s->f32, s->stream));
 #undef CREATE_TRY
     // chunked exchange: clean binned partitions whose row blocks split into
-    // ACSIM_XCHUNKS (default 4) chunks of whole source blocks; 0 or 1 keeps the unchunked sequence
+    // ACSIM_XCHUNKS chunks of whole source blocks AND of whole phase-B receiver blocks (chunk k's
+    // exchange is recorded after phase B's blocks [k*qpc, (k+1)*qpc), which must cover exactly the
+    // chunk's rows); 0 or 1 keeps the unchunked sequence.  Default: 4 for virtual partitions (GPU-
+    // tested bit-exact), and the per-round all-gather for a real multi-rank communicator until a
+    // multi-GPU run has matched the golden hash (the grouped send / receive path is opt-in there).
     if (partitioned && s->binned && s->clean) {
-        uint32_t K = 4;
+        uint32_t K = (comm_id && nranks > 1) ? 0u : 4u;
         if (const char* v = getenv("ACSIM_XCHUNKS")) K = (uint32_t)strtoul(v, nullptr, 10);
-        if (K >= 2 && K <= acs_sim::kMaxX && s->rows_per % ((uint64_t)K * bin_sa) == 0) s->xchunks = K;
+        if (K >= 2 && K <= acs_sim::kMaxX && s->rows_per % ((uint64_t)K * bin_sa) == 0 &&
+            (s->rows_per / K) % kBinSB == 0)
+            s->xchunks = K;
     }
     s->bin_sa = bin_sa;
     if (s->xchunks) {
@@ -1192,6 +1202,21 @@ extern "C" {
 int acs_abi_version(void) { return ACS_ABI_VERSION; }
 
 const char* acs_last_error(void) { return g_err.c_str(); }
+
+int acs_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return fail(ACS_EDEVICE, "hipGetDeviceCount failed");
+    return n;
+}
+
+int acs_runtime_info(char* out, uint64_t cap) {
+    if (!out || cap == 0) return fail(ACS_EINVAL, "acs_runtime_info: empty buffer");
+    int hv = 0, nv = 0;
+    if (hipRuntimeGetVersion(&hv) != hipSuccess) return fail(ACS_EDEVICE, "hipRuntimeGetVersion failed");
+    if (ncclGetVersion(&nv) != ncclSuccess) return fail(ACS_ECOMM, "ncclGetVersion failed");
+    snprintf(out, cap, "hip %d rccl %d", hv, nv);
+    return ACS_OK;
+}
 
 int acs_create(const acs_config* cfg, int backend, const int* devices, int n_devices, acs_sim** out) {
     if (out) *out = nullptr;

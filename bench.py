@@ -148,39 +148,27 @@ def load_pmc(kernel: str, n_nodes: int, dtype: str = "f64"):
 
 
 class Ctx:
-    """Rank / device / collective plumbing shared by the headline and the legs."""
+    """Rank / device / control-plane plumbing shared by the headline and the legs.  `group` is an
+    acsim.rendezvous.Group (plain sockets, no torch in the rank process: every rank maps only the
+    HIP runtime and RCCL libacsim.so was built against), None at N = 1."""
 
-    def __init__(self, world, rank, local_rank, dev, dist):
-        self.world, self.rank, self.local_rank, self.dev, self.dist = world, rank, local_rank, dev, dist
+    def __init__(self, world, rank, local_rank, dev, group):
+        self.world, self.rank, self.local_rank, self.dev, self.group = world, rank, local_rank, dev, group
 
     def barrier(self, sim=None):
         if sim is not None:
             sim.sync()
-        if self.dist is not None:
-            self.dist.barrier()
+        if self.group is not None:
+            self.group.barrier()
 
     def max(self, v: float) -> float:
-        if self.dist is None:
-            return float(v)
-        import torch
-        t = torch.tensor([float(v)], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
+        return float(v) if self.group is None else self.group.max(v)
 
     def all_ok(self, ok: bool) -> bool:
-        if self.dist is None:
-            return ok
-        import torch
-        t = torch.tensor([1 if ok else 0], dtype=torch.int64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
-        return bool(t.item())
+        return ok if self.group is None else self.group.min(1.0 if ok else 0.0) > 0.5
 
     def gather(self, obj):
-        if self.dist is None:
-            return [obj]
-        out = [None] * self.world
-        self.dist.all_gather_object(out, obj)
-        return out
+        return [obj] if self.group is None else self.group.all_gather(obj)
 
 
 def golden():
@@ -271,7 +259,7 @@ def leg_cfg5(ctx: Ctx, warm: int = 2, timed: int = 8) -> dict:
             sim = acsim.Simulator(cfg, device=ctx.dev)
         else:
             from acsim.distributed import partitioned_simulator
-            sim = partitioned_simulator(cfg, ctx.rank, ctx.world, ctx.dev)
+            sim = partitioned_simulator(cfg, ctx.rank, ctx.world, ctx.dev, group=ctx.group)
     except Exception as e:  # noqa: BLE001
         err = f"{type(e).__name__}: {e}"
     if not ctx.all_ok(err is None):
@@ -350,20 +338,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
+    group = None
     ndev = 1
+    import acsim
     if world > 1:
-        import torch  # imported before libacsim so both share one HIP runtime
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
-        ndev = max(1, torch.cuda.device_count())   # does not initialise the GPU on this image
+        # torch-free control plane (acsim/rendezvous.py): importing torch here would map torch's
+        # own HIP runtime and RCCL before libacsim.so and bind the library to them
+        from acsim.rendezvous import Group
+        group = Group.from_env()
+        ndev = max(1, acsim._abi.device_count())
         if world > ndev and not a.allow_shared_device:
             raise SystemExit(f"{world} ranks but {ndev} GPU(s): one rank per GPU (--allow-shared-device "
                              f"for a rehearsal that is not a scaling result)")
-    import acsim
 
     dev = local_rank % ndev
-    ctx = Ctx(world, rank, local_rank, dev, dist)
+    ctx = Ctx(world, rank, local_rank, dev, group)
     n = a.n_nodes
     cfg = acsim.preset("cfg4", n_nodes=n, max_rounds=a.warmup + a.steps, instance_offset=rank,
                        dtype=a.dtype)
@@ -377,6 +366,7 @@ def main():
     sim.round(a.steps)
     ctx.barrier(sim)
     dt = time.perf_counter() - t0
+    dt_local = dt
     k_ms, k_n, kname = sim.kernel_timing()
     sim.set_kernel_timing(False)
     rounds = int(sim.rounds()[0])
@@ -426,8 +416,15 @@ def main():
                            "cfg4.fixed100_x_sha256); null for other shapes (--dtype f32, --n-nodes)"},
     }
     if world > ndev:
+        # rehearsal: several ranks time replicas on one card; no aggregate is a throughput result
         out["shared_device"] = True
         out["ranks"] = world
+        out["rank_values"] = ctx.gather(n * a.steps / dt_local)
+        out["value"] = None
+        out["hbm_roofline_pct_wall"] = None
+    # which HIP runtime / RCCL each rank runs on (the N = 1 line records the same for comparison)
+    rt = ctx.gather(acsim._abi.runtime_info())
+    out["runtime"] = {"rank0": rt[0], "all_ranks_same": all(r == rt[0] for r in rt)}
     if rank == 0:
         out["roofline"]["traffic"] = load_pmc(kname, n, a.dtype)
 
@@ -448,8 +445,9 @@ def main():
     legs = [s for s in a.legs.split(",") if s]
     if legs:
         def watchdog():
+            # the headline line is printed, but the run must not look clean: exit non-zero
             emit(f"watchdog: legs unfinished after {a.leg_timeout:.0f} s")
-            os._exit(0)
+            os._exit(3)
         timer = threading.Timer(a.leg_timeout, watchdog)
         timer.daemon = True
         timer.start()
@@ -469,8 +467,9 @@ def main():
             out["cpu_baseline"] = None
             out["cpu_baseline_error"] = f"{type(e).__name__}: {e}"
     emit()
-    if dist is not None:
-        dist.destroy_process_group()
+    if group is not None:
+        group.barrier()
+        group.close()
 
 
 if __name__ == "__main__":

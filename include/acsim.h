@@ -222,6 +222,12 @@ int acs_get_kernel_timing(struct acs_sim* sim, double* total_ms, uint64_t* launc
 /* Wait for all device work of this handle. */
 int acs_sync(struct acs_sim* sim);
 
+/* Process-level facts for multi-GPU launchers (bench.py, acsim.rendezvous): the number of HIP
+ * devices visible (hipGetDeviceCount), and the HIP runtime and RCCL versions this library is
+ * running on, as "hip <hipRuntimeGetVersion> rccl <ncclGetVersion>" (NUL-terminated, cut to cap). */
+int acs_device_count(void);
+int acs_runtime_info(char* out, uint64_t cap);
+
 void acs_destroy(struct acs_sim* sim);
 const char* acs_last_error(void);
 int acs_abi_version(void);

@@ -131,3 +131,13 @@ def test_missing_library_fails_loudly(monkeypatch):
     monkeypatch.setattr(_abi, "LIB_PATH", "/nonexistent/libacsim.so")
     with pytest.raises(ImportError):
         _abi.load_library()
+
+
+def test_runtime_info_reports_the_rocm_libraries(acsim_lib):
+    """acs_runtime_info (no GPU needed): the HIP runtime and RCCL versions, and the files this
+    process mapped for them — bench.py records them per rank so an N > 1 run can be checked to
+    run on the same libraries as the single-GPU run and the GPU suite."""
+    info = _abi.runtime_info()
+    assert re.fullmatch(r"hip \d+ rccl \d+", info["versions"]), info
+    assert len(info["libamdhip64"]) == 1 and info["libamdhip64"][0].startswith("/opt/rocm"), info
+    assert len(info["librccl"]) == 1 and info["librccl"][0].startswith("/opt/rocm"), info

@@ -50,3 +50,36 @@ def test_sharded_equals_unsharded_gloo(tmp_path, oracle_mod, world):
     assert v["rounds_max"] == v["ref_rounds_max"]
     assert v["hist_total"] == 37
     assert v["max_over_ranks"] == world - 1
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_rendezvous_group_torch_free(tmp_path, oracle_mod, world):
+    """bench.py's control plane (acsim/rendezvous.py): all-gather, barrier, broadcast, max / min /
+    sum, and the sharded run's statistics reduction over plain sockets, launched by
+    torch.distributed.run like the driver's N > 1 bench; the workers never import torch."""
+    out = tmp_path / "verdict.json"
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(HERE, "rdzv_worker.py"), str(out)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    v = json.load(open(out))
+    assert v["world"] == world
+    assert v["gather_ok"] and v["broadcast_ok"]
+    assert v["max"] == world - 1 and v["min"] == 0
+    assert v["sum"] == [k * world * (world + 1) // 2 for k in range(4)]
+    assert v["rounds_equal"] and v["values_equal"]
+    assert v["n_instances"] == 37 and v["hist_total"] == 37
+    assert v["n_converged"] == v["ref_converged"]
+    assert v["node_rounds"] == v["ref_node_rounds"]
+    assert v["max_over_ranks"] == world - 1
+    assert not v["torch_imported"]
+
+
+def test_rendezvous_single_rank_is_local():
+    from acsim.rendezvous import Group
+    g = Group(0, 1)
+    assert g.all_gather(5) == [5] and g.max(2.0) == 2.0 and g.broadcast(b"x") == b"x"
+    g.barrier()
+    g.close()

@@ -71,6 +71,26 @@ def test_rccl_single_rank_path():
         assert np.array_equal(bits(p.spread_trace(0)), bits(ref.spread_trace(0)))
 
 
+def test_partitioned_simulator_through_rendezvous_group():
+    """bench.py's N > 1 code path up to the communicator: acsim.distributed.partitioned_simulator
+    with the torch-free control plane (acsim.rendezvous.Group, world 1): the RCCL id is made on
+    rank 0 and broadcast over the group, the communicator forms, and the run equals the plain one.
+    The process maps one HIP runtime and one RCCL, the ones libacsim.so was built against."""
+    from acsim.distributed import partitioned_simulator
+    from acsim.rendezvous import Group
+    cfg = preset("cfg5", n_nodes=1 << 17, max_rounds=10, trace_spread=True)
+    with Group(0, 1) as g:
+        with acsim.Simulator(cfg) as ref, partitioned_simulator(cfg, 0, 1, 0, group=g) as p:
+            ref.run()
+            p.run()
+            assert np.array_equal(p.rounds(), ref.rounds())
+            assert np.array_equal(bits(p.values(0)), bits(ref.values(0)))
+            assert np.array_equal(bits(p.spread_trace(0)), bits(ref.spread_trace(0)))
+    info = acsim._abi.runtime_info()
+    assert len(info["libamdhip64"]) == 1 and len(info["librccl"]) == 1, info
+    assert info["libamdhip64"][0].startswith("/opt/rocm"), info
+
+
 def test_partition_rejects_unsupported():
     with pytest.raises(acsim.AcsError):
         acsim.Simulator(preset("cfg2"), partitions=2)       # complete graph
@@ -121,6 +141,31 @@ def test_chunked_exchange_matches_unpartitioned(oracle_mod, parts, sa, chunks, m
             assert np.array_equal(bits(p.spread_trace(0)), bits(rt))
             for q in range(parts):
                 assert np.array_equal(bits(p.partition_values(q)), bits(rx)), f"copy {q} differs"
+
+
+@pytest.mark.parametrize("n,chunked", [(3000, False), (6144, True)])
+def test_chunked_exchange_small_source_blocks(oracle_mod, n, chunked):
+    """Source blocks of 64 senders (ACSIM_BIN_SA=64): the chunks must still be whole phase-B
+    receiver blocks (256 rows), else a chunk's exchange could be recorded before all of its rows
+    ran phase B.  N = 3000 over 2 partitions gives 384-row chunks (refused: the unchunked sequence
+    runs); N = 6144 gives 768-row chunks (chunked).  Both equal the unpartitioned run."""
+    cfg = preset("cfg5", n_nodes=n, termination="eps", eps=1e-7, max_rounds=200, trace_spread=True)
+    with env(ACSIM_BIN_SA=64):
+        with acsim.Simulator(cfg) as ref:
+            ref.run()
+            rr, rx, rt = ref.rounds(), ref.values(0), ref.spread_trace(0)
+        with env(ACSIM_XCHUNKS=4), acsim.Simulator(cfg, partitions=2) as p:
+            assert ("xchunks4" in p.kernel_name()) == chunked, p.kernel_name()
+            p.run()
+            assert np.array_equal(p.rounds(), rr)
+            assert np.array_equal(bits(p.values(0)), bits(rx))
+            assert np.array_equal(bits(p.spread_trace(0)), bits(rt))
+            for q in range(2):
+                assert np.array_equal(bits(p.partition_values(q)), bits(rx)), f"copy {q} differs"
+    with oracle_mod.OracleSimulator(cfg, threads=8) as o:
+        o.run()
+        assert np.array_equal(o.rounds(), rr)
+        assert np.array_equal(bits(o.values(0)), bits(rx))
 
 
 def test_chunked_exchange_single_rank_rccl():
