@@ -52,6 +52,8 @@ constexpr uint32_t kPolRevB = 8;       // phase B: each XCD walks its receiver-b
                                        // (the stage tiles phase A wrote last are read first)
 constexpr uint32_t kPolNoPf = 16;       // phase B (NP > 1): per-part descriptor loads instead of the prefetch
 constexpr uint32_t kPolBfPick = 32;     // phase B (NP > 1): branch-free pick-up (clamped read + select)
+constexpr uint32_t kPolSc1Store = 64;   // phase A / M: write-through (sc1) stage stores instead of nt: no
+                                        // dirty stage lines left in L2 for the kernel boundary to write back
 constexpr uint32_t kPolDefault = kPolNtStore | kPolNtInv | kPolBfPick;   // measured (cfg4): phase B 80 -> 71 (nt) -> 63.2 us (pick-up), phase A -1 us
 
 // ------------------------------------------------------------------------------ shared pieces
@@ -64,6 +66,23 @@ constexpr uint32_t kPolDefault = kPolNtStore | kPolNtInv | kPolBfPick;   // meas
 // batch paid a full store round trip.)
 __device__ __forceinline__ double2 bin_pair(double a, double b) { return make_double2(a, b); }
 __device__ __forceinline__ float2 bin_pair(float a, float b) { return make_float2(a, b); }
+
+// Write-through (sc1) 16- or 8-byte store through a buffer descriptor (MI355X guide, Guideline 16
+// R1 store form): the line leaves L2 with the store instead of staying dirty there.
+template <typename V2>
+__device__ __forceinline__ void bin_store_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t off, const V2& v) {
+    if constexpr (sizeof(V2) == 16) {
+        using UV = unsigned int __attribute__((ext_vector_type(4)));
+        UV bits;
+        __builtin_memcpy(&bits, &v, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(bits, rs, off, 0, 16);
+    } else {
+        using UV = unsigned int __attribute__((ext_vector_type(2)));
+        UV bits;
+        __builtin_memcpy(&bits, &v, 8);
+        __builtin_amdgcn_raw_buffer_store_b64(bits, rs, off, 0, 16);
+    }
+}
 
 template <typename V2>
 __device__ __forceinline__ void bin_store(V2* dst, const V2& v, bool nt) {
@@ -78,10 +97,12 @@ __device__ __forceinline__ void bin_store(V2* dst, const V2& v, bool nt) {
 }
 
 // VT = double, or float for fp32 plans (the instruction's store is then 8 bytes)
+// smode: 0 plain stores, 1 nontemporal, 2 write-through (sc1)
 template <typename VT = double>
 __device__ __forceinline__ void bin_stream(const VT* lx, const uint16_t* __restrict__ idx, VT* __restrict__ out,
-                                           uint64_t p0, uint64_t p1, bool nt_store = false) {
+                                           uint64_t p0, uint64_t p1, uint32_t smode = 0) {
     using V2 = decltype(bin_pair(VT(0), VT(0)));
+    const bool nt_store = smode == 1;
     constexpr uint32_t SUP = kBinA / 64 * 512, SUPW = SUP / 2;
     constexpr uint32_t SB = 1;   // super-steps per pipelined batch
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -101,6 +122,11 @@ __device__ __forceinline__ void bin_stream(const VT* lx, const uint16_t* __restr
         // (measured on cfg4: SB = 1 59-61 us, SB = 2 62, SB = 4 64; keeping the previous
         // super-step's stores in flight across the loop head — first indices consumed before the
         // loop — 67 us; the loop kept rolled 62 us)
+        // write-through stores go through a descriptor based at this range (offsets < 4 GiB)
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            out + p0, 0, (int)((p1 - p0) * sizeof(VT) < 0x7FFFFFF0ull ? (p1 - p0) * sizeof(VT) : 0x7FFFFFF0ull),
+            0x00020000);
+        const uint32_t ob = (w * 256 + lane) * (uint32_t)sizeof(V2);   // this lane's byte offset in a super-step
         for (uint64_t bi = 0; bi < nb; ++bi) {
             // next batch's indices (the last batch re-reads itself: no branch around the loads)
             const uint64_t bn = bi + 1 < nb ? bi + 1 : bi;
@@ -112,9 +138,13 @@ __device__ __forceinline__ void bin_stream(const VT* lx, const uint16_t* __restr
 #pragma unroll
             for (uint32_t u = 0; u < SB; ++u)
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    bin_store(op + (bi * SB + u) * SUPW + q * 64, bin_pair(lx[c[u][q] & 0xFFFFu], lx[c[u][q] >> 16]),
-                              nt_store);
+                for (int q = 0; q < 4; ++q) {
+                    const V2 v = bin_pair(lx[c[u][q] & 0xFFFFu], lx[c[u][q] >> 16]);
+                    if (smode == 2)
+                        bin_store_sc1(rs, ob + (uint32_t)(((bi * SB + u) * SUPW + q * 64) * sizeof(V2)), v);
+                    else
+                        bin_store(op + (bi * SB + u) * SUPW + q * 64, v, nt_store);
+                }
 #pragma unroll
             for (uint32_t u = 0; u < SB; ++u)
 #pragma unroll
@@ -258,7 +288,7 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
         __syncthreads();
     }
     const uint64_t t1 = ts ? __builtin_amdgcn_s_memrealtime() : 0;
-    bin_stream(lx, idxA, stage, p0, p1, (pol & kPolNtStore) != 0);
+    bin_stream(lx, idxA, stage, p0, p1, (pol & kPolSc1Store) ? 2u : (pol & kPolNtStore) ? 1u : 0u);
     if (ts) bin_ts(ts, t0, t1);
 }
 
@@ -279,7 +309,7 @@ __global__ __launch_bounds__(kBinA) void k_bin_regroup(const VT* __restrict__ st
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     bin_dma_runs(mt + (uint64_t)g * (PK + 1), w * PK / NW, (w + 1) * PK / NW, stage1, lm);
     __syncthreads();
-    bin_stream(lm, idxM, stage2, moff[g], moff[g + 1], (pol & kPolNtStore) != 0);
+    bin_stream(lm, idxM, stage2, moff[g], moff[g + 1], (pol & kPolSc1Store) ? 2u : (pol & kPolNtStore) ? 1u : 0u);
 }
 
 // ------------------------------------------------------------------------------ phase B
@@ -1130,7 +1160,7 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     p.ofree = ofree;
     {
         const char* v = getenv("ACSIM_BIN_POL");
-        p.pol = v ? (uint32_t)strtoul(v, nullptr, 0) & 63u : kPolDefault;
+        p.pol = v ? (uint32_t)strtoul(v, nullptr, 0) & 127u : kPolDefault;
     }
     if (ofree) {   // order-free phase B: receiver ids in image order
         p.rstride = ((uint32_t)d * kBinSB + p.nrun * (G.pad - 1) + 15u) & ~15u;
