@@ -36,201 +36,9 @@
 #include <mutex>
 #include <vector>
 
-#include "finalize.hpp"
-#include "resolve.hpp"
-#include "rules.hpp"
+#include "binned_dev.hpp"
 
 namespace acs {
-
-constexpr uint32_t kBinA = 512;        // phase-A / phase-M workgroup: 8 waves
-constexpr uint32_t kBinMCap = 19456;   // phase-M LDS image capacity (elements, 152 KiB)
-// cache-policy switches of the exchange (launch argument `pol`; ACSIM_BIN_POL overrides the default)
-constexpr uint32_t kPolNtRuns = 1;     // phase B: stage runs by nontemporal LDS-DMA
-constexpr uint32_t kPolNtStore = 2;    // phase A / M: nontemporal stage stores
-constexpr uint32_t kPolNtInv = 4;      // phase B: nontemporal invpos loads
-constexpr uint32_t kPolRevB = 8;       // phase B: each XCD walks its receiver-block range downwards
-                                       // (the stage tiles phase A wrote last are read first)
-constexpr uint32_t kPolNoPf = 16;       // phase B (NP > 1): per-part descriptor loads instead of the prefetch
-constexpr uint32_t kPolBfPick = 32;     // phase B (NP > 1): branch-free pick-up (clamped read + select)
-constexpr uint32_t kPolSc1Store = 64;   // phase A / M: write-through (sc1) stage stores instead of nt: no
-                                        // dirty stage lines left in L2 for the kernel boundary to write back
-constexpr uint32_t kPolDefault = kPolNtStore | kPolNtInv | kPolBfPick;   // measured (cfg4): phase B 80 -> 71 (nt) -> 63.2 us (pick-up), phase A -1 us
-
-// ------------------------------------------------------------------------------ shared pieces
-// Stream [p0, p1) of an index stream: out[p] = lds[idx[p]].  Super-steps of 512 positions per
-// wave; instruction q of a lane covers positions q*128 + 2*lane, +1 (one u32 of two indices, one
-// 16-byte store), so every wave-instruction reads 256 B and writes 1 KiB contiguously.
-// Software-pipelined by batches of SB super-steps: the index loads of batch k+1 are issued before
-// batch k's gathers and stores.  (gfx9 counts loads and stores in one in-order vmcnt: the plain
-// loop's wait for its index loads also waited for the previous batch's store completions, so each
-// batch paid a full store round trip.)
-__device__ __forceinline__ double2 bin_pair(double a, double b) { return make_double2(a, b); }
-__device__ __forceinline__ float2 bin_pair(float a, float b) { return make_float2(a, b); }
-
-// Write-through (sc1) 16- or 8-byte store through a buffer descriptor (MI355X guide, Guideline 16
-// R1 store form): the line leaves L2 with the store instead of staying dirty there.
-template <typename V2>
-__device__ __forceinline__ void bin_store_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t off, const V2& v) {
-    if constexpr (sizeof(V2) == 16) {
-        using UV = unsigned int __attribute__((ext_vector_type(4)));
-        UV bits;
-        __builtin_memcpy(&bits, &v, 16);
-        __builtin_amdgcn_raw_buffer_store_b128(bits, rs, off, 0, 16);
-    } else {
-        using UV = unsigned int __attribute__((ext_vector_type(2)));
-        UV bits;
-        __builtin_memcpy(&bits, &v, 8);
-        __builtin_amdgcn_raw_buffer_store_b64(bits, rs, off, 0, 16);
-    }
-}
-
-template <typename V2>
-__device__ __forceinline__ void bin_store(V2* dst, const V2& v, bool nt) {
-    if (nt) {   // as an integer vector of V2's size (the builtin takes native vector types)
-        using UV = unsigned int __attribute__((ext_vector_type(sizeof(V2) / 4)));
-        UV bits;
-        __builtin_memcpy(&bits, &v, sizeof(V2));
-        __builtin_nontemporal_store(bits, reinterpret_cast<UV*>(dst));
-    } else {
-        *dst = v;
-    }
-}
-
-// VT = double, or float for fp32 plans (the instruction's store is then 8 bytes)
-// smode: 0 plain stores, 1 nontemporal, 2 write-through (sc1)
-template <typename VT = double>
-__device__ __forceinline__ void bin_stream(const VT* lx, const uint16_t* __restrict__ idx, VT* __restrict__ out,
-                                           uint64_t p0, uint64_t p1, uint32_t smode = 0) {
-    using V2 = decltype(bin_pair(VT(0), VT(0)));
-    const bool nt_store = smode == 1;
-    constexpr uint32_t SUP = kBinA / 64 * 512, SUPW = SUP / 2;
-    constexpr uint32_t SB = 1;   // super-steps per pipelined batch
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint64_t p = p0;
-    if ((p0 & 1) == 0) {
-        const uint64_t nsup = (p1 - p0) / SUP;
-        const uint64_t nb = nsup / SB;
-        const uint32_t* ip = reinterpret_cast<const uint32_t*>(idx + p0) + w * 256 + lane;
-        V2* op = reinterpret_cast<V2*>(out + p0) + w * 256 + lane;
-        uint32_t c[SB][4];
-        if (nb) {
-#pragma unroll
-            for (uint32_t u = 0; u < SB; ++u)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) c[u][q] = __builtin_nontemporal_load(ip + u * SUPW + q * 64);
-        }
-        // (measured on cfg4: SB = 1 59-61 us, SB = 2 62, SB = 4 64; keeping the previous
-        // super-step's stores in flight across the loop head — first indices consumed before the
-        // loop — 67 us; the loop kept rolled 62 us)
-        // write-through stores go through a descriptor based at this range (offsets < 4 GiB)
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            out + p0, 0, (int)((p1 - p0) * sizeof(VT) < 0x7FFFFFF0ull ? (p1 - p0) * sizeof(VT) : 0x7FFFFFF0ull),
-            0x00020000);
-        const uint32_t ob = (w * 256 + lane) * (uint32_t)sizeof(V2);   // this lane's byte offset in a super-step
-        for (uint64_t bi = 0; bi < nb; ++bi) {
-            // next batch's indices (the last batch re-reads itself: no branch around the loads)
-            const uint64_t bn = bi + 1 < nb ? bi + 1 : bi;
-            uint32_t cn[SB][4];
-#pragma unroll
-            for (uint32_t u = 0; u < SB; ++u)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) cn[u][q] = __builtin_nontemporal_load(ip + (bn * SB + u) * SUPW + q * 64);
-#pragma unroll
-            for (uint32_t u = 0; u < SB; ++u)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const V2 v = bin_pair(lx[c[u][q] & 0xFFFFu], lx[c[u][q] >> 16]);
-                    if (smode == 2)
-                        bin_store_sc1(rs, ob + (uint32_t)(((bi * SB + u) * SUPW + q * 64) * sizeof(V2)), v);
-                    else
-                        bin_store(op + (bi * SB + u) * SUPW + q * 64, v, nt_store);
-                }
-#pragma unroll
-            for (uint32_t u = 0; u < SB; ++u)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) c[u][q] = cn[u][q];
-        }
-        for (uint64_t k = nb * SB; k < nsup; ++k) {   // the last < SB super-steps
-            uint32_t cc[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) cc[q] = __builtin_nontemporal_load(ip + k * SUPW + q * 64);
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                bin_store(op + k * SUPW + q * 64, bin_pair(lx[cc[q] & 0xFFFFu], lx[cc[q] >> 16]), nt_store);
-        }
-        p = p0 + nsup * SUP;
-    }
-    for (uint64_t q = p + threadIdx.x; q < p1; q += blockDim.x) out[q] = lx[idx[q]];
-}
-
-// Copy runs [r0, r1) of a run table (start in `src` elements, element offset `pre` in the LDS
-// image; run k ends where run k+1's image begins) into LDS by 16-byte LDS-DMA.  Every run is
-// padded to an even length, so starts are 16-byte aligned on both sides.  Descriptors are fetched
-// one per lane, 64 at a time, and broadcast with readlane: no run waits on a dependent load.
-// Runs are padded to EPU = 16 / sizeof(VT) elements (2 for fp64, 4 for fp32).
-template <typename VT = double>
-__device__ __forceinline__ void bin_dma_runs(const uint2* __restrict__ tb, uint32_t r0, uint32_t r1,
-                                             const VT* __restrict__ src, VT* dst, bool nt = false,
-                                             uint32_t base = 0) {   // base: image offset of dst[0]
-    constexpr uint32_t EPU = 16 / sizeof(VT);
-    const uint32_t lane = threadIdx.x & 63;
-    const uint4* s16 = reinterpret_cast<const uint4*>(src);
-    uint4* d16 = reinterpret_cast<uint4*>(dst);
-    for (uint32_t g = r0; g < r1; g += 64) {
-        const uint32_t ng = r1 - g < 64 ? r1 - g : 64;
-        uint2 dsc = make_uint2(0u, 0u);
-        uint32_t nxt = 0;
-        if (lane < ng) {
-            dsc = tb[g + lane];
-            nxt = tb[g + lane + 1].y;
-        }
-        for (uint32_t k = 0; k < ng; ++k) {
-            const uint32_t so = __builtin_amdgcn_readlane(dsc.x, k);
-            const uint32_t pre = __builtin_amdgcn_readlane(dsc.y, k);
-            const uint32_t n16 = (__builtin_amdgcn_readlane(nxt, k) - pre) / EPU;   // 16-byte units
-            const uint4* sp = s16 + so / EPU + lane;
-            uint4* dp = d16 + (pre - base) / EPU;
-            if (nt) {   // once-read runs: nontemporal policy (aux = 2)
-                for (uint32_t o = 0; o < n16; o += 64)
-                    if (o + lane < n16) __builtin_amdgcn_global_load_lds(sp + o, dp + o, 16, 0, 2);
-            } else {
-                for (uint32_t o = 0; o < n16; o += 64)
-                    if (o + lane < n16) __builtin_amdgcn_global_load_lds(sp + o, dp + o, 16, 0, 0);
-            }
-        }
-    }
-}
-
-// The same copy for runs [r0, r1) of a block of at most 64 runs whose descriptors the wave already
-// holds one per lane (dsc = tb[lane], nxt = tb[lane + 1].y): no load before the first DMA.
-template <typename VT = double>
-__device__ __forceinline__ void bin_dma_runs_pf(uint2 dsc, uint32_t nxt, uint32_t r0, uint32_t r1,
-                                                const VT* __restrict__ src, VT* dst, uint32_t base) {
-    constexpr uint32_t EPU = 16 / sizeof(VT);
-    const uint32_t lane = threadIdx.x & 63;
-    const uint4* s16 = reinterpret_cast<const uint4*>(src);
-    uint4* d16 = reinterpret_cast<uint4*>(dst);
-    for (uint32_t k = r0; k < r1; ++k) {
-        const uint32_t so = __builtin_amdgcn_readlane(dsc.x, k);
-        const uint32_t pre = __builtin_amdgcn_readlane(dsc.y, k);
-        const uint32_t n16 = (__builtin_amdgcn_readlane(nxt, k) - pre) / EPU;
-        const uint4* sp = s16 + so / EPU + lane;
-        uint4* dp = d16 + (pre - base) / EPU;
-        for (uint32_t o = 0; o < n16; o += 64)
-            if (o + lane < n16) __builtin_amdgcn_global_load_lds(sp + o, dp + o, 16, 0, 0);
-    }
-}
-
-// diagnostic (ACSIM_BIN_TS): workgroup entry, end of its staging wait, end, in 100 MHz ticks
-__device__ __forceinline__ void bin_ts(uint64_t* ts, uint64_t t0, uint64_t t1) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
-        ts[3 * blockIdx.x] = t0;
-        ts[3 * blockIdx.x + 1] = t1;
-        ts[3 * blockIdx.x + 2] = t2;
-    }
-}
 
 // ------------------------------------------------------------------------------ phase A
 template <typename VT = double>
@@ -349,13 +157,6 @@ __global__ __launch_bounds__(256) void k_bin_tag(const VT* __restrict__ x, const
         xt[j + k] = mode ? bin_tag_value(id, mode, VT(0)) : x[j + k];
     }
 }
-
-// NP-pass phase B (NP > 1, ACSIM_BIN_SPLIT=NP): block b's image is copied in NP parts (runs
-// [k*nrun/NP, (k+1)*nrun/NP)) through an LDS buffer of kBinPartCap<D, NP> elements; after each
-// part's DMA every lane picks up the values whose invpos falls in that part.  1/NP of the LDS per
-// workgroup: more resident workgroups per CU.  The plan enables it only when every part fits.
-template <int D, int NP>
-constexpr uint32_t kBinPartCap = D * kBinSB / NP + D * kBinSB / 16;   // + 1/16 of the image: run-length variation and padding
 
 // VAR: a CSR graph padded to D (§8(f) row 1): slots t >= deg(i) are absent entries, slot numbers
 // are rowptr[i] + t (one drop draw each); single pass only.
