@@ -916,6 +916,8 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     if (cfg->topology == ACS_TOPO_COMPLETE && s->N <= kBatchedMaxN && cfg->delay_max == 0) {
         s->path = PATH_BATCHED;
         s->kname = batched_small_name((uint32_t)s->N, cfg->rule, cfg->fault_model != ACS_FAULT_NONE);
+        if (const uint32_t F = batched_split_factor((uint32_t)s->N, cfg->rule, cfg->fault_model != ACS_FAULT_NONE); F > 1)
+            s->kname = "k_batched_split<" + std::to_string(F) + ">";
         const char* env = getenv("ACSIM_MFMA");
         s->mfma = !(env && env[0] == '0') && !s->f32 &&
                   batched_mfma_supported((uint32_t)s->N, cfg->rule, cfg->fault_model != ACS_FAULT_NONE, cfg->mask_group,

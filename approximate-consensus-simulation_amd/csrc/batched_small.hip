@@ -284,6 +284,137 @@ __global__ __launch_bounds__(64, (!SORT && !FAULTS) ? ACS_BATCHED_WPE : 1) void 
     }
 }
 
+// ------------------------------------------------------------------------------ split instances
+// cfg3 (N = 64, AVERAGE, no fault schedule) with F lanes per receiver: one instance = F waves of one
+// workgroup; wave w holds receivers [w*R, (w+1)*R) (R = 64/F), lane l of it receiver w*R + l % R,
+// part f = l / R.  Why: at one wave per instance the batch is dealt in whole-instance units, and
+// a shard of 12 500 instances fills 3.05 generations of the resident waves (the fourth nearly
+// empty); F lanes per receiver make the unit 1/F of an instance's time.
+// Per round and lane:
+//   - Philox calls [f*16/F, (f+1)*16/F) of receiver i's drop slots (64/F drop bits); the F parts'
+//     bits are all-gathered over the F lanes of the receiver by lane shuffles;
+//   - the §A.7 tree restricted to entries j ≡ f (mod F): the stride-halving tree over 64 entries
+//     first combines the residue classes mod F as a stride-halving tree over the F class sums
+//     ((c0 + c2) + (c1 + c3) at F = 4), and each class sum is the same tree over its 64/F entries
+//     (adjacent pairs over bit-reversed order, as average_tree_sel); the F lanes then combine the
+//     class sums in that order by shuffles, so every lane holds the spec's sum bit for bit;
+//   - honest (min, max) by wave shuffles and an LDS word per wave; x through LDS.
+template <int F, bool OMIT, typename VT, int... Q>
+__device__ __forceinline__ VT class_tree(const VT* xs, uint32_t f, VT xi, uint64_t usexi, uint64_t use0,
+                                         std::integer_sequence<int, Q...>) {
+    constexpr int L = 64 / F;
+    constexpr int LOG2L = ilog2(L);
+    VT acc[LOG2L + 1];
+    const uint64_t u = usexi >> f, z = use0 >> f;   // bit F*k: entry F*k + f
+    const uint32_t w0 = (uint32_t)u, w1 = (uint32_t)(u >> 32), z0 = (uint32_t)z, z1 = (uint32_t)(z >> 32);
+    const VT* xf = xs + f;
+    auto leaf = [&](int k) -> VT {   // entry F*k + f
+        const int bit = F * k;
+        VT v = xf[bit];
+        if constexpr (OMIT) v = bitsel((uint32_t)__builtin_amdgcn_sbfe((int)(bit < 32 ? z0 : z1), bit & 31, 1), VT(0), v);
+        return bitsel((uint32_t)__builtin_amdgcn_sbfe((int)(bit < 32 ? w0 : w1), bit & 31, 1), xi, v);
+    };
+    auto fence = [](int q) {
+        if ((q & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+    };
+    ((push_leaf<L, Q, LOG2L>(acc, leaf(bitrev<LOG2L>(Q))), fence(Q)), ...);
+    return acc[LOG2L];
+}
+
+template <int F, typename VT>
+__device__ __forceinline__ VT shfl_xor_v(VT v, int m) {
+    return __shfl_xor(v, m, 64);
+}
+
+template <int F, typename VT = double>
+__global__ __launch_bounds__(64 * F) void k_batched_split(const BatchArgs a, uint32_t kmax) {
+    constexpr int R = 64 / F;        // receivers per wave
+    constexpr int CPL = 16 / F;      // Philox calls (4 slots each) per lane and round
+    const uint32_t lb = blockIdx.x;
+    InstState* S = a.st + lb;
+    if (S->done) return;
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t f = lane / R, i = w * R + lane % R;
+    const MsgParams& mp = a.mp;
+    uint32_t r = S->rounds;
+    double lo = S->lo, hi = S->hi, spread = S->spread;
+    const uint32_t b = (uint32_t)(mp.inst_offset + lb);
+    const uint32_t bG = b - b % mp.mask_group;
+    const VT* xin = reinterpret_cast<const VT*>((r & 1u) ? a.x1 : a.x0) + (uint64_t)lb * 64;
+    VT xi = xin[i];
+    __shared__ VT xs[64];
+    __shared__ double2 red[F];
+    bool done = false, conv = spread <= a.eps;
+    for (uint32_t q = 0; q < kmax; ++q) {
+        __syncthreads();   // the previous round's reads of xs and red are done
+        if (f == 0) xs[i] = xi;
+        __syncthreads();
+        uint64_t miss = 0;
+        if (mp.thr) {   // drop bits of entries [f*4*CPL, (f+1)*4*CPL) of receiver i, then all-gathered
+            uint32_t m = 0;
+#pragma unroll
+            for (int g = 0; g < CPL; ++g) {
+                const U4 wd = philox10(i * 16u + f * CPL + g, r, bG, kStreamDrop, mp.key);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) m = shift_in_lt(m, wd.v[e], mp.thr);
+            }
+            miss = (uint64_t)(__builtin_bitreverse32(m) >> (32 - 4 * CPL)) << (f * 4 * CPL);
+#pragma unroll
+            for (int sh = R; sh < 64; sh <<= 1) {
+                const uint32_t lo32 = (uint32_t)__shfl_xor((int)(uint32_t)miss, sh, 64);
+                const uint32_t hi32 = (uint32_t)__shfl_xor((int)(uint32_t)(miss >> 32), sh, 64);
+                miss |= (uint64_t)hi32 << 32 | lo32;
+            }
+        }
+        miss &= ~(1ull << i);   // the self entry is never missing
+        constexpr auto seq = std::make_integer_sequence<int, 64 / F>{};
+        VT c = mp.omit ? class_tree<F, true>(xs, f, xi, 0ull, miss, seq) : class_tree<F, false>(xs, f, xi, miss, 0ull, seq);
+#pragma unroll
+        for (int st = F / 2; st >= 1; st >>= 1) {   // stride-halving over the class sums
+            const VT o = shfl_xor_v<F>(c, st * R);
+            c = (f & st) ? o + c : c + o;
+        }
+        const uint32_t mn_ = mp.omit ? 64u - (uint32_t)__builtin_popcountll(miss) : 64u;
+        xi = c / (VT)mn_;
+        r += 1;
+        const double wmn = wave_min((double)xi), wmx = wave_max((double)xi);
+        if (lane == 0) red[w] = make_double2(wmn, wmx);
+        __syncthreads();
+        lo = red[0].x;
+        hi = red[0].y;
+#pragma unroll
+        for (int k = 1; k < F; ++k) {
+            lo = __builtin_fmin(lo, red[k].x);
+            hi = __builtin_fmax(hi, red[k].y);
+        }
+        spread = (double)((VT)hi - (VT)lo);   // binary32 subtraction in fp32 mode
+        if (a.trace && threadIdx.x == 0) a.trace[(uint64_t)lb * a.trace_stride + r] = spread;
+        conv = spread <= a.eps;
+        done = (a.term_eps && conv) || r >= a.max_rounds;
+        if (done) break;
+    }
+    VT* xout = reinterpret_cast<VT*>((r & 1u) ? a.x1 : a.x0) + (uint64_t)lb * 64;
+    if (f == 0) xout[i] = xi;
+    if (threadIdx.x == 0) {
+        S->lo = lo;
+        S->hi = hi;
+        S->spread = spread;
+        S->rounds = r;
+        S->converged = conv ? 1u : 0u;
+        S->done = done ? 1u : 0u;
+        if (done) atomicAdd(a.n_done, 1u);
+    }
+}
+
+// Lanes per receiver for a clean AVERAGE batch of 64-node instances: ACSIM_BATCH_SPLIT (1, 2, 4)
+// or the default.
+uint32_t batched_split_factor(uint32_t N, uint32_t rule, bool faults) {
+    if (N != 64 || rule != 0 || faults) return 1;
+    uint32_t F = 1;
+    if (const char* v = getenv("ACSIM_BATCH_SPLIT")) F = (uint32_t)strtoul(v, nullptr, 10);
+    return F == 2 || F == 4 ? F : 1;
+}
+
 static int pick_p(uint32_t N) {
     int P = 2;
     while ((uint32_t)P < N) P <<= 1;
@@ -320,6 +451,15 @@ static hipError_t launch_batched_small_t(const BatchArgs& a, uint64_t B, uint32_
 
 hipError_t launch_batched_small(const BatchArgs& a, uint64_t B, uint32_t k, hipStream_t s) {
     if (a.N < 1 || a.N > kBatchedMaxN) return hipErrorNotSupported;
+    const uint32_t F = batched_split_factor(a.N, a.rule, a.status != nullptr);
+    if (F > 1) {
+        const dim3 grid((unsigned)B), block(64 * F);
+        if (F == 2 && a.f32) hipLaunchKernelGGL((k_batched_split<2, float>), grid, block, 0, s, a, k);
+        else if (F == 2) hipLaunchKernelGGL((k_batched_split<2, double>), grid, block, 0, s, a, k);
+        else if (a.f32) hipLaunchKernelGGL((k_batched_split<4, float>), grid, block, 0, s, a, k);
+        else hipLaunchKernelGGL((k_batched_split<4, double>), grid, block, 0, s, a, k);
+        return hipGetLastError();
+    }
     return a.f32 ? launch_batched_small_t<float>(a, B, k, s) : launch_batched_small_t<double>(a, B, k, s);
 }
 

@@ -299,5 +299,7 @@ bool batched_mfma_supported(uint32_t N, uint32_t rule, bool faults, uint32_t mas
 hipError_t launch_batched_mfma(const BatchArgs& a, uint64_t B, uint32_t k, hipStream_t s);
 hipError_t launch_batched_small(const BatchArgs& a, uint64_t B, uint32_t k, hipStream_t s);
 const char* batched_small_name(uint32_t N, uint32_t rule, bool faults);
+// lanes per receiver of the clean AVERAGE N = 64 batch (k_batched_split<F>; 1 = k_batched_small)
+uint32_t batched_split_factor(uint32_t N, uint32_t rule, bool faults);
 
 }  // namespace acs
