@@ -160,13 +160,18 @@ __global__ __launch_bounds__(256) void k_bin_tag(const VT* __restrict__ x, const
 
 // VAR: a CSR graph padded to D (§8(f) row 1): slots t >= deg(i) are absent entries, slot numbers
 // are rowptr[i] + t (one drop draw each); single pass only.
-// Faulty NP > 1: the parts' LDS buffers admit 4 workgroups per CU, so ask for 4 waves per SIMD (at
-// most 128 VGPRs; unbounded the faulty instantiations take 163-179 and run 3 workgroups per CU)
-#ifndef ACS_FAULTY_WPE
-#define ACS_FAULTY_WPE 4
+// Faulty NP > 1: the parts' LDS buffers admit 4 workgroups per CU, but the faulty bodies need more
+// than the 128 VGPRs of 4 waves per SIMD (bounded to 4 they spilled 148-312 B/lane of scratch).
+// The cfg4_byz shape (t = 5, not W-MSR) needs 163 with the drop mask drawn up front: 3 waves per
+// SIMD (168 VGPRs), no scratch.  W-MSR and t = 0 (full 33-value sorts) need up to 203: 2.
+// ACS_FAULTY_WPE overrides (variant builds).
+#ifdef ACS_FAULTY_WPE
+#define ACS_FAULTY_WPE_OF(T, W) ACS_FAULTY_WPE
+#else
+#define ACS_FAULTY_WPE_OF(T, W) ((T) == 5 && !(W) ? 3 : 2)
 #endif
 template <int D, int T, bool WMSR = false, bool FAULTY = false, typename VT = double, int NP = 1, bool VAR = false>
-__global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE : 1) void k_bin_gather(const RoundArgs a, const VT* __restrict__ stage,
+__global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) : 1) void k_bin_gather(const RoundArgs a, const VT* __restrict__ stage,
                                                        const uint16_t* __restrict__ invpos,
                                                        const uint2* __restrict__ tiles, uint32_t nrun, uint32_t Q,
                                                        uint32_t Qc, uint32_t pol) {
@@ -222,6 +227,36 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE : 1) void
         if (live) {
             dg = a.deg[i];
             if constexpr (FAULTY) rp = a.rowptr[i];
+        }
+    }
+    // §A.5 drop decisions of the lane's D slots as a bit mask, drawn before the values arrive: the
+    // Philox state is then dead while the D + 1 values are live (drawn inside the resolution loop
+    // below, the faulty two-pass kernels spilled 36-49 VGPRs at their 128-VGPR bound, and the CSR
+    // slot loop — one draw per slot — was too large to unroll, so v[] went to scratch)
+    uint32_t dmask = 0;
+    if constexpr (FAULTY) {
+        static_assert(D <= 32, "one drop bit per slot in a 32-bit mask");
+        const MsgParams& mp = a.mp;
+        if (mp.thr && live) {
+            const uint32_t bI = (uint32_t)mp.inst_offset, bG = bI - bI % mp.mask_group;
+            if constexpr (!VAR) {
+#pragma unroll
+                for (int q = 0; q < D / 4; ++q) {
+                    const U4 w = philox10((uint32_t)i * (uint32_t)(D / 4) + q, a.r, bG, kStreamDrop, mp.key);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) dmask |= (uint32_t)(w.v[e] < mp.thr) << (4 * q + e);
+                }
+            } else if (dg) {   // slots rowptr[i] .. + deg(i) - 1: one call per 4 consecutive slots
+                const uint64_t c1 = (rp + dg + 3) >> 2;
+                for (uint64_t c = rp >> 2; c < c1; ++c) {
+                    const U4 w = philox10((uint32_t)c, a.r, bG, kStreamDrop, mp.key);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const uint64_t t = 4 * c + e - rp;   // wraps past 2^64 below rp: out of range
+                        if (t < dg) dmask |= (uint32_t)(w.v[e] < mp.thr) << t;
+                    }
+                }
+            }
         }
     }
     uint4 ip[D / 8];
@@ -285,7 +320,10 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE : 1) void
                     const uint32_t p0 = wd[e] & 0xFFFFu, p1 = wd[e] >> 16;
                     const bool in0 = (k == 0 || p0 >= lo) && (k + 1 == (uint32_t)NP || p0 < hi);
                     const bool in1 = (k == 0 || p1 >= lo) && (k + 1 == (uint32_t)NP || p1 < hi);
-                    if (pol & kPolBfPick) {   // every lane reads (offset 0 when out of this part), then selects
+                    // (faulty kernels: exec-masked reads straight into v; the clamped read + select
+                    // holds the old and the new values together: 148-312 B/lane of scratch at their
+                    // 128-VGPR bound)
+                    if (!FAULTY && (pol & kPolBfPick)) {   // every lane reads (offset 0 when out of this part), then selects
                         const VT t0 = raw[in0 ? p0 - lo : 0u], t1 = raw[in1 ? p1 - lo : 0u];
                         v[1 + 8 * q + 2 * e] = in0 ? t0 : v[1 + 8 * q + 2 * e];
                         v[2 + 8 * q + 2 * e] = in1 ? t1 : v[2 + 8 * q + 2 * e];
@@ -314,14 +352,11 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE : 1) void
             }
             if constexpr (FAULTY) {   // §A.5 drops, §A.4 / §A.6 sender resolution (round_regular.hip order)
                 const MsgParams& mp = a.mp;
-                const uint32_t bI = (uint32_t)mp.inst_offset, bG = bI - bI % mp.mask_group;
+                const uint32_t bI = (uint32_t)mp.inst_offset;
                 const uint32_t r = a.r, iu = (uint32_t)i;
                 const VT lo = (VT)S->lo, hi = (VT)S->hi;
 #pragma unroll
                 for (int q = 0; q < D / 4; ++q) {
-                    U4 w;
-                    w.v[0] = w.v[1] = w.v[2] = w.v[3] = 0xFFFFFFFFu;
-                    if (!VAR && mp.thr) w = philox10(iu * (uint32_t)(D / 4) + q, r, bG, kStreamDrop, mp.key);
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const int t = 4 * q + e;
@@ -331,8 +366,7 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE : 1) void
                             continue;
                         }
                         const uint64_t slot = VAR ? rp + t : (uint64_t)iu * D + t;
-                        const bool dropped = VAR ? (mp.thr && draw(mp.key, kStreamDrop, bG, r, slot) < mp.thr)
-                                                 : w.v[e] < mp.thr;
+                        const bool dropped = (dmask >> t) & 1u;
                         VT u = v[1 + t];
                         uint32_t stj = kHonest;
                         if constexpr (sizeof(VT) == 8) {
