@@ -207,7 +207,8 @@ __device__ __forceinline__ void sg_sync(uint32_t* cnt, uint32_t& epoch) {
 
 constexpr uint32_t kSubBytes = 36864;                  // one sub-group's LDS part buffer (kBinPartCap<32, 2>)
 constexpr uint32_t kSubCtl = 4 * kSubBytes;            // sub-group control words after the 4 buffers
-constexpr uint32_t kPersistLds = kSubCtl + 4 * 64;     // B-worker LDS; the A-worker needs SA*8 + 128
+constexpr uint32_t kSubCtlStride = 32;                 // u32 words of control per sub-group (128 B)
+constexpr uint32_t kPersistLds = kSubCtl + 4 * kSubCtlStride * 4;   // B-worker LDS; the A-worker needs SA*8 + 128
 
 // One receiver block b of round rr.  Returns false when the worker must stop (the run ended, or
 // the watchdog fired).
@@ -222,7 +223,7 @@ __device__ bool persist_block(const PersistArgs& a, const Ctl& c, unsigned char*
     const uint32_t tl = tid & 255, wv = tl >> 6, lane = tid & 63;
     const uint32_t g = __builtin_amdgcn_readfirstlane(tid >> 8);   // sub-group (wave-uniform)
     double* raw = reinterpret_cast<double*>(smem + g * kSubBytes);
-    uint32_t* sbar = reinterpret_cast<uint32_t*>(smem + kSubCtl) + g * 16;
+    uint32_t* sbar = reinterpret_cast<uint32_t*>(smem + kSubCtl) + g * kSubCtlStride;
     volatile uint32_t* sflag = sbar + 1;
     double2* red = reinterpret_cast<double2*>(sbar + 4);
     const uint32_t P = a.P;
@@ -432,8 +433,9 @@ __device__ bool persist_block(const PersistArgs& a, const Ctl& c, unsigned char*
 template <int D, int T, bool WMSR, int NP>
 __device__ void persist_b(const PersistArgs& a, unsigned char* smem) {
     const uint32_t g = threadIdx.x >> 8;                       // sub-group
-    // per sub-group control words: [0] barrier count, [1] go flag, [4..11] the 4 waves' (min, max)
-    if ((threadIdx.x & 255) == 0) reinterpret_cast<uint32_t*>(smem + kSubCtl)[g * 16] = 0;
+    // per sub-group control words: [0] barrier count, [1] go flag, [4..19] the 4 waves' (min, max)
+    static_assert(4 + 4 * 4 <= kSubCtlStride, "a sub-group's control words");
+    if ((threadIdx.x & 255) == 0) reinterpret_cast<uint32_t*>(smem + kSubCtl)[g * kSubCtlStride] = 0;
     __syncthreads();
     uint32_t epoch = 0;
     const Ctl c = ctl_of(a);

@@ -52,15 +52,16 @@ def test_split_matches_oracle(oracle_mod, name, F):
         assert g.kernel_name() == f"k_batched_split<{F}>", g.kernel_name()
         g.run()
         gx, gr = g.all_values(), g.rounds()
-        gt = np.stack([g.spread_trace(b) for b in range(min(cfg.n_instances, 8))])
+        gt = [g.spread_trace(b) for b in range(min(cfg.n_instances, 8))]
     with oracle_mod.OracleSimulator(cfg, threads=8) as o:
         o.run()
         ox, orr = o.all_values(), o.rounds()
-        ot = np.stack([o.spread_trace(b) for b in range(min(cfg.n_instances, 8))])
+        ot = [o.spread_trace(b) for b in range(min(cfg.n_instances, 8))]
     u = np.uint32 if cfg.dtype == "f32" else np.uint64
     assert np.array_equal(gr, orr)
     assert np.array_equal(np.ascontiguousarray(gx).view(u), np.ascontiguousarray(ox).view(u))
-    assert np.array_equal(gt.view(np.uint64), ot.view(np.uint64))
+    for a, b in zip(gt, ot):   # (instances stop at different rounds: traces differ in length)
+        assert np.array_equal(a.view(np.uint64), b.view(np.uint64))
 
 
 @pytest.mark.parametrize("F", [2, 4])
