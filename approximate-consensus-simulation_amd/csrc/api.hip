@@ -91,6 +91,8 @@ struct acs_sim {
     uint32_t* h_ndone = nullptr;   // pinned [2]
     RunSummary* dsum = nullptr;    // acs_run's summary, folded on the device
     RunSummary* h_sum = nullptr;   // pinned copy
+    bool want_summary = false;     // acs_run on a one-launch path: enqueue the summary before the sync
+    bool summary_ready = false;    // h_sum holds the summary of the current state
     uint32_t round = 0;            // round of every unfinished instance
     bool all_done = false;
     // node partitioning: rank owns rows [rank*rows_per, (rank+1)*rows_per) ∩ [0, N)
@@ -700,6 +702,11 @@ static int advance(acs_sim* s, uint32_t k) {
             HIP_TRY(launch_batched_small(a, s->B, k, s->stream));
         if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
         HIP_TRY(hipMemcpyAsync(s->h_ndone, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+        if (s->want_summary) {   // acs_run: the result summary rides on the same synchronisation
+            HIP_TRY(launch_run_summary(s->st, s->B, s->dsum, s->stream));
+            HIP_TRY(hipMemcpyAsync(s->h_sum, s->dsum, sizeof(RunSummary), hipMemcpyDeviceToHost, s->stream));
+            s->summary_ready = true;
+        }
         HIP_TRY(hipStreamSynchronize(s->stream));
         s->round += k;
         s->all_done = s->h_ndone[0] == s->B;
@@ -1365,14 +1372,20 @@ int acs_run(acs_sim* s, acs_result* out) {
     if (!s) return fail(ACS_EINVAL, "null sim");
     HIP_TRY(hipSetDevice(s->device));
     const auto t0 = std::chrono::steady_clock::now();
+    s->want_summary = out != nullptr;
+    s->summary_ready = false;
     int rc = advance(s, s->c.max_rounds);
+    s->want_summary = false;
     if (rc) return rc;
-    HIP_TRY(hipStreamSynchronize(s->stream));
+    if (!s->summary_ready) HIP_TRY(hipStreamSynchronize(s->stream));
     const auto t1 = std::chrono::steady_clock::now();
     if (out) {   // the summary is folded on the device: 32 bytes back instead of B states
-        HIP_TRY(launch_run_summary(s->st, s->B, s->dsum, s->stream));
-        HIP_TRY(hipMemcpyAsync(s->h_sum, s->dsum, sizeof(RunSummary), hipMemcpyDeviceToHost, s->stream));
-        HIP_TRY(hipStreamSynchronize(s->stream));
+        if (!s->summary_ready) {
+            HIP_TRY(launch_run_summary(s->st, s->B, s->dsum, s->stream));
+            HIP_TRY(hipMemcpyAsync(s->h_sum, s->dsum, sizeof(RunSummary), hipMemcpyDeviceToHost, s->stream));
+            HIP_TRY(hipStreamSynchronize(s->stream));
+        }
+        s->summary_ready = false;
         const RunSummary& r = *s->h_sum;
         memset(out, 0, sizeof *out);
         out->n_instances = s->B;

@@ -326,8 +326,12 @@ __device__ __forceinline__ VT shfl_xor_v(VT v, int m) {
     return __shfl_xor(v, m, 64);
 }
 
+#ifndef ACS_SPLIT_WPE
+#define ACS_SPLIT_WPE 0   // variant builds: waves per SIMD asked of the fp64 F = 2 kernel (unbounded: 98 VGPRs, 4)
+#endif
 template <int F, typename VT = double>
-__global__ __launch_bounds__(64 * F) void k_batched_split(const BatchArgs a, uint32_t kmax) {
+__global__ __launch_bounds__(64 * F, (F == 2 && sizeof(VT) == 8 && ACS_SPLIT_WPE) ? ACS_SPLIT_WPE : 1) void k_batched_split(
+    const BatchArgs a, uint32_t kmax) {
     constexpr int R = 64 / F;        // receivers per wave
     constexpr int CPL = 16 / F;      // Philox calls (4 slots each) per lane and round
     const uint32_t lb = blockIdx.x;
@@ -410,7 +414,9 @@ __global__ __launch_bounds__(64 * F) void k_batched_split(const BatchArgs a, uin
 // or the default.
 uint32_t batched_split_factor(uint32_t N, uint32_t rule, bool faults) {
     if (N != 64 || rule != 0 || faults) return 1;
-    uint32_t F = 1;
+    // default 2: at 10^5 instances as fast as one lane per receiver (2.08 ms either way), and the
+    // 8-rank shard's tail shrinks (0.300 -> 0.281 ms); 4 costs 26 % more work (profiles/r03_s02_cfg3_split.jsonl)
+    uint32_t F = 2;
     if (const char* v = getenv("ACSIM_BATCH_SPLIT")) F = (uint32_t)strtoul(v, nullptr, 10);
     return F == 2 || F == 4 ? F : 1;
 }
