@@ -217,6 +217,8 @@ struct PersistPlan {
     uint64_t* ctl = nullptr;                   // [nctl] control words, zeroed before every launch
     uint32_t nctl = 0;
     uint64_t tmo = 0;                          // watchdog per wait, s_memrealtime ticks (100 MHz)
+    uint64_t* ts = nullptr;                    // ACSIM_PERSIST_TS diagnostic buffer (PersistArgs::ts)
+    uint32_t ts_k = 0;                         // rounds it holds
 };
 struct PersistArgs {
     const uint16_t* idxA;
@@ -234,6 +236,8 @@ struct PersistArgs {
     uint64_t N, tmo;
     uint32_t SA, P, Q, S, NA, NB, r0, k, max_rounds, term_eps, rule;
     double eps;
+    uint64_t* ts;           // diagnostic (ACSIM_PERSIST_TS=<file>): [k][NA][3] A-worker (wait start,
+                            // staged, stream end) then [k][Q][3] block (poll start, ready, done), 100 MHz
 };
 // S = 0: choose; returns hipErrorNotSupported when the plan / device does not fit the scheme.
 hipError_t persist_build(PersistPlan& pp, const BinnedPlan& p, uint64_t N, uint32_t d, uint32_t trim, uint32_t rule,

@@ -164,6 +164,8 @@ __device__ void persist_a(const PersistArgs& a, unsigned char* smem) {
     const uint32_t nbA = (uint32_t)((base + n + kBinSB - 1) / kBinSB - base / kBinSB);   // receiver blocks of a's rows
     for (uint32_t rr = 0; rr < a.k; ++rr) {
         const uint32_t r = a.r0 + rr;
+        uint64_t* tsa = a.ts ? a.ts + ((uint64_t)rr * a.NA + w) * 3 : nullptr;
+        if (tsa && threadIdx.x == 0) tsa[0] = now_ticks();
         if (threadIdx.x < kPW) lprog[threadIdx.x] = 0;
         if (threadIdx.x == 0) {
             uint32_t stop = 0;
@@ -189,7 +191,9 @@ __device__ void persist_a(const PersistArgs& a, unsigned char* smem) {
                 if (o + threadIdx.x < n16) __builtin_amdgcn_global_load_lds(xs + o, ld + o, 16, 0, 16);
         }
         __syncthreads();
+        if (tsa && threadIdx.x == 0) tsa[1] = now_ticks();
         persist_stream(lx, a.idxA, a.stage[r & 1], p0, p1, c.prog + w, (uint64_t)(rr + 1) << 32, lprog);
+        if (tsa && threadIdx.x == 0) tsa[2] = now_ticks();
     }
 }
 
@@ -236,6 +240,8 @@ __device__ bool persist_block(const PersistArgs& a, const Ctl& c, unsigned char*
         pdsc = tb[lane];
         pnxt = tb[lane + 1].y;
     }
+    uint64_t* tsb = a.ts ? a.ts + ((uint64_t)a.k * a.NA + (uint64_t)rr * a.Q + b) * 3 : nullptr;
+    if (tsb && tl == 0) tsb[0] = now_ticks();
     // wave 0 waits for the previous round's verdict and for every source block's stream to pass
     // this block's tile; the sub-group learns the outcome through sflag
     if (wv == 0) {
@@ -268,6 +274,7 @@ __device__ bool persist_block(const PersistArgs& a, const Ctl& c, unsigned char*
     }
     sg_sync(sbar, epoch);
     if (!*sflag) return false;
+    if (tsb && tl == 0) tsb[1] = now_ticks();
 
     const uint32_t nrun = P;
     const uint64_t li = (uint64_t)b * kBinSB + tl;   // receiver
@@ -378,6 +385,7 @@ __device__ bool persist_block(const PersistArgs& a, const Ctl& c, unsigned char*
     }
     // every wave's x stores (and wave 0's partial) drained, then one lane signals
     sg_sync(sbar, epoch);
+    if (tsb && tl == 0) tsb[2] = now_ticks();
     if (wv == 0) {
         uint32_t last = 0;
         if (lane == 0) {
@@ -465,6 +473,7 @@ __global__ __launch_bounds__(kPT, 1) void k_bin_persist(const PersistArgs a) {
 
 // ------------------------------------------------------------------------------ host side
 void persist_free(PersistPlan& pp) {
+    (void)hipFree(pp.ts);
     (void)hipFree(pp.aseg);
     (void)hipFree(pp.stage2);
     (void)hipFree(pp.partial2);
@@ -568,9 +577,54 @@ hipError_t launch_round_persist(const PersistPlan& pp, const BinnedPlan& p, cons
     hipError_t e = hipMemsetAsync(pp.ctl, 0, (uint64_t)pp.nctl * sizeof(uint64_t), s);
     if (e != hipSuccess) return e;
     PersistArgs aa = a;
+    const char* tsf = getenv("ACSIM_PERSIST_TS");
+    const uint64_t nts = 3ull * a.k * ((uint64_t)pp.NA + a.Q);
+    if (tsf && a.k) {   // diagnostic timeline of this launch (the last launch's is left in the file)
+        PersistPlan& mp = const_cast<PersistPlan&>(pp);
+        if (mp.ts_k < a.k) {
+            (void)hipFree(mp.ts);
+            mp.ts = nullptr;
+            if ((e = hipMalloc(&mp.ts, nts * sizeof(uint64_t))) != hipSuccess) return e;
+            mp.ts_k = a.k;
+        }
+        if ((e = hipMemsetAsync(mp.ts, 0, nts * sizeof(uint64_t), s)) != hipSuccess) return e;
+        aa.ts = mp.ts;
+    } else {
+        aa.ts = nullptr;
+    }
     void* args[] = {&aa};
     const dim3 grid(pp.NA + pp.NB), block(kPT);
     const bool w = a.rule == 4;
+    if (aa.ts) {   // launch, wait, dump: kind,round,index,t0,t1,t2
+        hipError_t le = hipErrorNotSupported;
+#define X(DD, TT, NPP)                                                                                             \
+        if (d == DD && trim == TT)                                                                                 \
+            le = hipLaunchCooperativeKernel(w ? reinterpret_cast<const void*>(k_bin_persist<DD, TT, DD != 32, NPP>) \
+                                              : reinterpret_cast<const void*>(k_bin_persist<DD, TT, false, NPP>), \
+                                            grid, block, args, kPersistLds, s);
+        ACS_PERSIST_VARIANTS(X)
+#undef X
+        if (le != hipSuccess) return le;
+        std::vector<uint64_t> h(nts);
+        if ((e = hipMemcpyAsync(h.data(), aa.ts, nts * 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        if (FILE* f = fopen(tsf, "w")) {
+            for (uint32_t rr = 0; rr < a.k; ++rr)
+                for (uint32_t q = 0; q < pp.NA; ++q) {
+                    const uint64_t* t = h.data() + ((uint64_t)rr * pp.NA + q) * 3;
+                    fprintf(f, "A,%u,%u,%llu,%llu,%llu\n", rr, q, (unsigned long long)t[0], (unsigned long long)t[1],
+                            (unsigned long long)t[2]);
+                }
+            for (uint32_t rr = 0; rr < a.k; ++rr)
+                for (uint32_t q = 0; q < a.Q; ++q) {
+                    const uint64_t* t = h.data() + ((uint64_t)a.k * pp.NA + (uint64_t)rr * a.Q + q) * 3;
+                    fprintf(f, "B,%u,%u,%llu,%llu,%llu\n", rr, q, (unsigned long long)t[0], (unsigned long long)t[1],
+                            (unsigned long long)t[2]);
+                }
+            fclose(f);
+        }
+        return hipSuccess;
+    }
 #define X(DD, TT, NPP)                                                                                             \
     if (d == DD && trim == TT)                                                                                     \
         return hipLaunchCooperativeKernel(w ? reinterpret_cast<const void*>(k_bin_persist<DD, TT, DD != 32, NPP>)   \

@@ -49,7 +49,7 @@ CASES = {
 def test_split_matches_oracle(oracle_mod, name, F):
     cfg = CASES[name]
     with env(ACSIM_BATCH_SPLIT=F), acsim.Simulator(cfg, device=0) as g:
-        assert g.kernel_name() == f"k_batched_split<{F}>", g.kernel_name()
+        assert g.kernel_name().startswith(f"k_batched_split<{F}>"), g.kernel_name()
         g.run()
         gx, gr = g.all_values(), g.rounds()
         gt = [g.spread_trace(b) for b in range(min(cfg.n_instances, 8))]
