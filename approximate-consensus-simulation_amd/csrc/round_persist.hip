@@ -99,8 +99,7 @@ __device__ __forceinline__ bool instance_done(const InstState* st) {
 // ------------------------------------------------------------------------------ A-worker
 // Stream [p0, p1) of idxA into `out` (write-through), 16 waves, progress published in `prog` as
 // tag | position (every position below it written and drained).  A wave records in lprog[w] how
-// many super-steps of its slices are drained (the s_waitcnt below leaves only the 4 index loads
-// just issued in flight); wave 0 publishes the minimum over the waves.
+// many super-steps of its slices are drained; wave 0 publishes the minimum over the waves.
 __device__ void persist_stream(const double* lx, const uint16_t* __restrict__ idx, double* __restrict__ out,
                                uint64_t p0, uint64_t p1, uint64_t* prog, uint64_t tag, volatile uint32_t* lprog) {
     constexpr uint32_t SUPW = kAPos / 2;
@@ -123,9 +122,13 @@ __device__ void persist_stream(const double* lx, const uint16_t* __restrict__ id
         uint32_t cn[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) cn[q] = __builtin_nontemporal_load(ip + bn * SUPW + q * 64);
-        // everything older than those 4 loads has completed: this wave's stores of super-steps < bi
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        lprog[w] = (uint32_t)bi;
+        // Issue order per super-step j: index loads of j + 1, then the stores of j.  Leaving the 12
+        // youngest operations (loads of bi and bi + 1, stores of bi - 1) in flight completes the
+        // stores of super-steps < bi - 1: the same wait the gathers of bi need anyway for their
+        // index loads, so up to two super-steps of stores stay in flight.  (Waiting for the stores
+        // of bi - 1 here — one super-step in flight — halved the stream: 170 µs per half block.)
+        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        lprog[w] = bi ? (uint32_t)bi - 1u : 0u;
         if (w == 0) {
             uint32_t m = lane < kPW ? lprog[lane] : 0xFFFFFFFFu;
 #pragma unroll
@@ -369,26 +372,23 @@ __device__ bool persist_block(const PersistArgs& a, const Ctl& c, unsigned char*
             }
         }
     }
-    // block (min, max) partial: waves -> LDS -> wave 0
+    // block (min, max) partial: waves -> LDS -> wave 0; the barrier also drains every wave's x stores
     mn = wave_min(mn);
     mx = wave_max(mx);
     if (lane == 0) red[wv] = make_double2(mn, mx);
-    sg_sync(sbar, epoch);
-    if (wv == 0 && lane == 0) {
-        double p = red[0].x, q = red[0].y;
-#pragma unroll
-        for (int k = 1; k < 4; ++k) {
-            p = __builtin_fmin(p, red[k].x);
-            q = __builtin_fmax(q, red[k].y);
-        }
-        store_partial_sc1(a.partial[r & 1] + b, make_double2(p, q));
-    }
-    // every wave's x stores (and wave 0's partial) drained, then one lane signals
     sg_sync(sbar, epoch);
     if (tsb && tl == 0) tsb[2] = now_ticks();
     if (wv == 0) {
         uint32_t last = 0;
         if (lane == 0) {
+            double p = red[0].x, q = red[0].y;
+#pragma unroll
+            for (int k = 1; k < 4; ++k) {
+                p = __builtin_fmin(p, red[k].x);
+                q = __builtin_fmax(q, red[k].y);
+            }
+            store_partial_sc1(a.partial[r & 1] + b, make_double2(p, q));
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the partial, before the signals
             __hip_atomic_fetch_add(c.cntb + (uint32_t)(((uint64_t)b * kBinSB) / a.SA), 1ull, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
             const uint64_t old = __hip_atomic_fetch_add(c.cntr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
