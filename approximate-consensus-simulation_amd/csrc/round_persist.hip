@@ -101,7 +101,8 @@ __device__ __forceinline__ bool instance_done(const InstState* st) {
 // tag | position (every position below it written and drained).  A wave records in lprog[w] how
 // many super-steps of its slices are drained; wave 0 publishes the minimum over the waves.
 __device__ void persist_stream(const double* lx, const uint16_t* __restrict__ idx, double* __restrict__ out,
-                               uint64_t p0, uint64_t p1, uint64_t* prog, uint64_t tag, volatile uint32_t* lprog) {
+                               uint64_t p0, uint64_t p1, uint64_t* prog, uint64_t tag, volatile uint32_t* lprog,
+                               uint32_t diag) {
     constexpr uint32_t SUPW = kAPos / 2;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t nsup = (p1 - p0) / kAPos;
@@ -142,9 +143,17 @@ __device__ void persist_stream(const double* lx, const uint16_t* __restrict__ id
                 if (lane == 0) st_sc1(prog, tag | (p0 + (uint64_t)m * kAPos));
             }
         }
+        if (diag & 1) {   // timing diagnostic only: nontemporal stores carry no publication guarantee
+            double2* op = reinterpret_cast<double2*>(out + p0) + w * 256 + lane;
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-            bin_store_sc1(rs, ob + (uint32_t)((bi * SUPW + q * 64) * 16), make_double2(lx[c[q] & 0xFFFFu], lx[c[q] >> 16]));
+            for (int q = 0; q < 4; ++q)
+                bin_store(op + bi * SUPW + q * 64, make_double2(lx[c[q] & 0xFFFFu], lx[c[q] >> 16]), true);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                bin_store_sc1(rs, ob + (uint32_t)((bi * SUPW + q * 64) * 16),
+                              make_double2(lx[c[q] & 0xFFFFu], lx[c[q] >> 16]));
+        }
 #pragma unroll
         for (int q = 0; q < 4; ++q) c[q] = cn[q];
     }
@@ -195,7 +204,7 @@ __device__ void persist_a(const PersistArgs& a, unsigned char* smem) {
         }
         __syncthreads();
         if (tsa && threadIdx.x == 0) tsa[1] = now_ticks();
-        persist_stream(lx, a.idxA, a.stage[r & 1], p0, p1, c.prog + w, (uint64_t)(rr + 1) << 32, lprog);
+        persist_stream(lx, a.idxA, a.stage[r & 1], p0, p1, c.prog + w, (uint64_t)(rr + 1) << 32, lprog, a.diag);
         if (tsa && threadIdx.x == 0) tsa[2] = now_ticks();
     }
 }
@@ -577,6 +586,7 @@ hipError_t launch_round_persist(const PersistPlan& pp, const BinnedPlan& p, cons
     hipError_t e = hipMemsetAsync(pp.ctl, 0, (uint64_t)pp.nctl * sizeof(uint64_t), s);
     if (e != hipSuccess) return e;
     PersistArgs aa = a;
+    if (const char* dv = getenv("ACSIM_PERSIST_DIAG")) aa.diag = (uint32_t)strtoul(dv, nullptr, 0);
     const char* tsf = getenv("ACSIM_PERSIST_TS");
     const uint64_t nts = 3ull * a.k * ((uint64_t)pp.NA + a.Q);
     if (tsf && a.k) {   // diagnostic timeline of this launch (the last launch's is left in the file)
