@@ -748,7 +748,7 @@ static int advance(acs_sim* s, uint32_t k) {
         RoctxRange range("acs: persistent binned rounds");
         HIP_TRY(launch_round_persist(s->pers, s->bin, a, s->d, s->c.trim, s->stream));
         if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
-        uint64_t* abort_word = s->pers.ctl + s->pers.NA + s->bin.P + 2;
+        uint64_t* abort_word = s->pers.ctl + persist_ctl_abort(s->pers, s->bin.P);
         HIP_TRY(hipMemcpyAsync(s->h_ndone, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(hipMemcpyAsync(&s->pers_abort, abort_word, sizeof(uint64_t), hipMemcpyDeviceToHost, s->stream));
         HIP_TRY(hipStreamSynchronize(s->stream));

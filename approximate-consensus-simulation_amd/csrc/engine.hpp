@@ -247,8 +247,10 @@ hipError_t persist_build(PersistPlan& pp, const BinnedPlan& p, uint64_t N, uint3
 void persist_free(PersistPlan& pp);
 hipError_t launch_round_persist(const PersistPlan& pp, const BinnedPlan& p, const PersistArgs& a, uint32_t d,
                                 uint32_t trim, hipStream_t s);
-// ctl word offsets
-inline uint32_t persist_ctl_cntb(const PersistPlan& pp) { return pp.NA; }
+// ctl layout (round_persist.hip): [S * kPersistNch) chunk counters, [P) receiver blocks done per
+// source block, blocks done, folds done, abort
+constexpr uint32_t kPersistNch = 32;
+inline uint64_t persist_ctl_abort(const PersistPlan& pp, uint32_t P) { return (uint64_t)pp.S * kPersistNch + P + 2; }
 
 // Generic kernel: one workgroup per receiver, LDS bitonic sort (any topology, m <= 8192).
 constexpr uint32_t kGenericMaxM = 8192;   // receivers with more entries take the big-m path

@@ -38,11 +38,15 @@ namespace {
 constexpr uint32_t kPT = 1024;           // threads per workgroup (16 waves, one workgroup per CU)
 constexpr uint32_t kPW = kPT / 64;       // waves
 constexpr uint32_t kAPos = 512 * kPW;    // stream positions per super-step (each wave 512)
+constexpr uint32_t kNch = kPersistNch;   // readiness chunks per segment (receiver-block ranges)
 
-// ctl layout: [0, NA) progress, [NA, NA+P) receiver blocks done per source block, then
-// NA+P: blocks done, +1: folds done, +2: abort
+// ctl layout: [0, S*kNch) streams done per (segment, chunk) — every source block's A-worker adds 1
+// when its stream has written and drained a chunk's tiles; then [P) receiver blocks done per
+// source block, blocks done, folds done, abort.  One word per wait: B-workers poll the chunk word
+// of their block (polling a progress word per source block — 64 sc1 loads per block and poll —
+// cost more fabric bandwidth than the round itself moved).
 struct Ctl {
-    uint64_t* prog;
+    uint64_t* chunk;
     uint64_t* cntb;
     uint64_t* cntr;
     uint64_t* vcnt;
@@ -50,13 +54,15 @@ struct Ctl {
 };
 __device__ __forceinline__ Ctl ctl_of(const PersistArgs& a) {
     Ctl c;
-    c.prog = a.ctl;
-    c.cntb = a.ctl + a.NA;
-    c.cntr = a.ctl + a.NA + a.P;
+    c.chunk = a.ctl;
+    c.cntb = a.ctl + (uint64_t)a.S * kNch;
+    c.cntr = c.cntb + a.P;
     c.vcnt = c.cntr + 1;
     c.abort = c.cntr + 2;
     return c;
 }
+// receiver blocks per chunk of a segment of Qs blocks
+__device__ __forceinline__ uint32_t chunk_blocks(uint32_t Qs) { return (Qs + kNch - 1) / kNch; }
 
 __device__ __forceinline__ uint64_t ld_sc1(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -97,12 +103,13 @@ __device__ __forceinline__ bool instance_done(const InstState* st) {
 }
 
 // ------------------------------------------------------------------------------ A-worker
-// Stream [p0, p1) of idxA into `out` (write-through), 16 waves, progress published in `prog` as
-// tag | position (every position below it written and drained).  A wave records in lprog[w] how
-// many super-steps of its slices are drained; wave 0 publishes the minimum over the waves.
+// Stream [p0, p1) of idxA into `out` (write-through), 16 waves.  A wave records in lprog[w] how
+// many super-steps of its slices are drained; wave 0 turns the minimum over the waves into a stream
+// position and, for every chunk whose tiles end at or below it (lane q of wave 0 holds chunk q's
+// end position cend, nch chunks), adds 1 to that chunk's counter.
 __device__ void persist_stream(const double* lx, const uint16_t* __restrict__ idx, double* __restrict__ out,
-                               uint64_t p0, uint64_t p1, uint64_t* prog, uint64_t tag, volatile uint32_t* lprog,
-                               uint32_t diag) {
+                               uint64_t p0, uint64_t p1, uint64_t* chunkc, uint64_t cend, uint32_t nch,
+                               volatile uint32_t* lprog, uint32_t diag) {
     constexpr uint32_t SUPW = kAPos / 2;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t nsup = (p1 - p0) / kAPos;
@@ -111,7 +118,17 @@ __device__ void persist_stream(const double* lx, const uint16_t* __restrict__ id
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(out + p0, 0, (int)(bytes < 0x7FFFFFF0ull ? bytes : 0x7FFFFFF0ull), 0x00020000);
     const uint32_t ob = (w * 256 + lane) * 16u;
-    uint32_t pub = 0;
+    uint32_t pub = 0, pubc = 0;   // super-steps / chunks published (wave 0)
+    // wave 0: publish the chunks whose tiles end at or below position pos
+    auto publish = [&](uint64_t pos) {
+        const uint32_t n = (uint32_t)__builtin_popcountll(__ballot(lane < nch && cend <= pos));
+        if (n > pubc) {
+            if (lane >= pubc && lane < n)
+                __hip_atomic_fetch_add(chunkc + lane, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            pubc = n;
+        }
+    };
+    if (w == 0) publish(p0);   // chunks with no tiles in this stream
     uint32_t c[4];
     if (nsup) {
 #pragma unroll
@@ -140,7 +157,7 @@ __device__ void persist_stream(const double* lx, const uint16_t* __restrict__ id
             m = __builtin_amdgcn_readfirstlane(m);
             if (m > pub) {
                 pub = m;
-                if (lane == 0) st_sc1(prog, tag | (p0 + (uint64_t)m * kAPos));
+                publish(p0 + (uint64_t)m * kAPos);
             }
         }
         if (diag & 1) {   // timing diagnostic only: nontemporal stores carry no publication guarantee
@@ -160,7 +177,7 @@ __device__ void persist_stream(const double* lx, const uint16_t* __restrict__ id
     for (uint64_t q = p0 + nsup * kAPos + threadIdx.x; q < p1; q += kPT) st_sc1(out + q, lx[idx[q]]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) st_sc1(prog, tag | p1);
+    if (w == 0) publish(p1);
 }
 
 __device__ void persist_a(const PersistArgs& a, unsigned char* smem) {
@@ -174,6 +191,17 @@ __device__ void persist_a(const PersistArgs& a, unsigned char* smem) {
     const uint64_t base = (uint64_t)src * a.SA;
     const uint32_t n = (uint32_t)(a.N - base < a.SA ? a.N - base : a.SA);
     const uint32_t nbA = (uint32_t)((base + n + kBinSB - 1) / kBinSB - base / kBinSB);   // receiver blocks of a's rows
+    // chunk q of this segment: receiver blocks [b0 + q*QC, b0 + (q+1)*QC); lane q of wave 0 holds the
+    // stream position where the chunk's tiles end (the start of the next block's tile of source src)
+    const uint32_t Qs = (a.Q + a.S - 1) / a.S, QC = chunk_blocks(Qs);
+    const uint32_t b0 = seg * Qs, b1 = b0 + Qs < a.Q ? b0 + Qs : a.Q;
+    const uint32_t nch = b1 > b0 ? (b1 - b0 + QC - 1) / QC : 0;
+    uint64_t cend = p1;
+    {
+        const uint32_t q = threadIdx.x & 63, e = b0 + (q + 1) * QC;
+        if (threadIdx.x < 64 && q < nch && e < b1) cend = a.tiles[(uint64_t)e * (a.P + 1) + src].x & ~1u;
+    }
+    uint64_t* chunkc = c.chunk + (uint64_t)seg * kNch;
     for (uint32_t rr = 0; rr < a.k; ++rr) {
         const uint32_t r = a.r0 + rr;
         uint64_t* tsa = a.ts ? a.ts + ((uint64_t)rr * a.NA + w) * 3 : nullptr;
@@ -204,7 +232,7 @@ __device__ void persist_a(const PersistArgs& a, unsigned char* smem) {
         }
         __syncthreads();
         if (tsa && threadIdx.x == 0) tsa[1] = now_ticks();
-        persist_stream(lx, a.idxA, a.stage[r & 1], p0, p1, c.prog + w, (uint64_t)(rr + 1) << 32, lprog, a.diag);
+        persist_stream(lx, a.idxA, a.stage[r & 1], p0, p1, chunkc, cend, nch, lprog, a.diag);
         if (tsa && threadIdx.x == 0) tsa[2] = now_ticks();
     }
 }
@@ -269,17 +297,15 @@ __device__ bool persist_block(const PersistArgs& a, const Ctl& c, unsigned char*
             }
             if (go && instance_done(a.st)) go = 0;
         }
-        if (go) {
-            const uint64_t need = ((uint64_t)(rr + 1) << 32) | (uint64_t)((pdsc.x & ~1u) + (pnxt - pdsc.y));
-            const uint64_t* pp = c.prog + (uint64_t)seg * P + (lane < P ? lane : 0);
-            while (true) {
-                const bool ok = lane >= P || ld_sc1(pp) >= need;
-                if (__builtin_amdgcn_read_exec() == __ballot(ok)) break;
+        if (go) {   // every source block's stream has drained this block's chunk
+            const uint64_t need = (uint64_t)P * (rr + 1);
+            const uint64_t* cw = c.chunk + (uint64_t)seg * kNch + (b - seg * Qs) / chunk_blocks(Qs);
+            while (__builtin_amdgcn_readfirstlane((uint32_t)(ld_sc1(cw) >= need)) == 0u) {
                 if (give_up(c, t0, a.tmo)) {
                     go = 0;
                     break;
                 }
-                __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_s_sleep(4);
             }
         }
         if (lane == 0) *sflag = go;
@@ -540,7 +566,7 @@ hipError_t persist_build(PersistPlan& pp, const BinnedPlan& p, uint64_t N, uint3
     as[(uint64_t)p.P * S] = p.Ep1;
     for (uint64_t k = 0; k + 1 < as.size(); ++k)
         if (as[k] > as[k + 1] || (as[k] & 1)) return hipErrorNotSupported;   // A order, even starts
-    pp.nctl = (pp.NA + p.P + 4 + 1) & ~1u;
+    pp.nctl = (uint32_t)((persist_ctl_abort(pp, p.P) + 1 + 1) & ~1ull);   // through the abort word, even
     e = hipMalloc(&pp.aseg, as.size() * sizeof(uint64_t));
     if (e == hipSuccess) e = hipMemcpy(pp.aseg, as.data(), as.size() * sizeof(uint64_t), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&pp.stage2, p.Ep1 * sizeof(double));
