@@ -280,7 +280,7 @@ __device__ bool persist_block(const PersistArgs& a, const Ctl& c, unsigned char*
         pdsc = tb[lane];
         pnxt = tb[lane + 1].y;
     }
-    uint64_t* tsb = a.ts ? a.ts + ((uint64_t)a.k * a.NA + (uint64_t)rr * a.Q + b) * 3 : nullptr;
+    uint64_t* tsb = a.ts ? a.ts + (uint64_t)a.k * a.NA * 3 + ((uint64_t)rr * a.Q + b) * 5 : nullptr;
     if (tsb && tl == 0) tsb[0] = now_ticks();
     // wave 0 waits for the previous round's verdict and for every source block's stream to pass
     // this block's tile; the sub-group learns the outcome through sflag
@@ -366,6 +366,7 @@ __device__ bool persist_block(const PersistArgs& a, const Ctl& c, unsigned char*
             }
         }
         sg_sync(sbar, epoch);   // this part's runs are in LDS
+        if (tsb && tl == 0) tsb[k == 0 ? 2 : 3] = now_ticks();
 #pragma unroll
         for (int q = 0; q < D / 8; ++q) {
             const uint32_t wd[4] = {ip[q].x, ip[q].y, ip[q].z, ip[q].w};
@@ -412,7 +413,7 @@ __device__ bool persist_block(const PersistArgs& a, const Ctl& c, unsigned char*
     mx = wave_max(mx);
     if (lane == 0) red[wv] = make_double2(mn, mx);
     sg_sync(sbar, epoch);
-    if (tsb && tl == 0) tsb[2] = now_ticks();
+    if (tsb && tl == 0) tsb[4] = now_ticks();
     if (wv == 0) {
         uint32_t last = 0;
         if (lane == 0) {
@@ -614,7 +615,7 @@ hipError_t launch_round_persist(const PersistPlan& pp, const BinnedPlan& p, cons
     PersistArgs aa = a;
     if (const char* dv = getenv("ACSIM_PERSIST_DIAG")) aa.diag = (uint32_t)strtoul(dv, nullptr, 0);
     const char* tsf = getenv("ACSIM_PERSIST_TS");
-    const uint64_t nts = 3ull * a.k * ((uint64_t)pp.NA + a.Q);
+    const uint64_t nts = 3ull * a.k * pp.NA + 5ull * a.k * a.Q;
     if (tsf && a.k) {   // diagnostic timeline of this launch (the last launch's is left in the file)
         PersistPlan& mp = const_cast<PersistPlan&>(pp);
         if (mp.ts_k < a.k) {
@@ -653,9 +654,10 @@ hipError_t launch_round_persist(const PersistPlan& pp, const BinnedPlan& p, cons
                 }
             for (uint32_t rr = 0; rr < a.k; ++rr)
                 for (uint32_t q = 0; q < a.Q; ++q) {
-                    const uint64_t* t = h.data() + ((uint64_t)a.k * pp.NA + (uint64_t)rr * a.Q + q) * 3;
-                    fprintf(f, "B,%u,%u,%llu,%llu,%llu\n", rr, q, (unsigned long long)t[0], (unsigned long long)t[1],
-                            (unsigned long long)t[2]);
+                    const uint64_t* t = h.data() + (uint64_t)a.k * pp.NA * 3 + ((uint64_t)rr * a.Q + q) * 5;
+                    fprintf(f, "B,%u,%u,%llu,%llu,%llu,%llu,%llu\n", rr, q, (unsigned long long)t[0],
+                            (unsigned long long)t[1], (unsigned long long)t[4], (unsigned long long)t[2],
+                            (unsigned long long)t[3]);
                 }
             fclose(f);
         }
