@@ -236,8 +236,9 @@ struct PersistArgs {
     uint64_t N, tmo;
     uint32_t SA, P, Q, S, NA, NB, r0, k, max_rounds, term_eps, rule;
     double eps;
-    uint32_t diag;          // diagnostic switches (ACSIM_PERSIST_DIAG, timing only): bit 0 = A stream
-                            // stores nontemporal instead of write-through (no publication guarantee)
+    uint32_t diag;          // diagnostic switches (ACSIM_PERSIST_DIAG, timing only, no publication
+                            // guarantee): bit 0 = A stream stores nontemporal instead of write-through,
+                            // bit 1 = B run copies by default-policy instead of sc1 LDS-DMA
     uint64_t* ts;           // diagnostic (ACSIM_PERSIST_TS=<file>): [k][NA][3] A-worker (wait start,
                             // staged, stream end) then [k][Q][3] block (poll start, ready, done), 100 MHz
 };

@@ -330,7 +330,10 @@ __device__ bool persist_block(const PersistArgs& a, const Ctl& c, unsigned char*
             const uint4* sp = s16 + so / 2 + lane;
             uint4* dp = d16 + pre / 2;
             for (uint32_t o = 0; o < n16; o += 64)
-                if (o + lane < n16) __builtin_amdgcn_global_load_lds(sp + o, dp + o, 16, 0, 16);
+                if (o + lane < n16) {
+                    if (a.diag & 2) __builtin_amdgcn_global_load_lds(sp + o, dp + o, 16, 0, 0);
+                    else __builtin_amdgcn_global_load_lds(sp + o, dp + o, 16, 0, 16);
+                }
         }
     }
     const double xi = live ? ld_sc1(a.x[r & 1] + li) : 0.0;
@@ -362,7 +365,10 @@ __device__ bool persist_block(const PersistArgs& a, const Ctl& c, unsigned char*
                 const uint4* sp = s16 + so / 2 + lane;
                 uint4* dp = d16 + (pre - lo) / 2;
                 for (uint32_t o = 0; o < n16; o += 64)
-                    if (o + lane < n16) __builtin_amdgcn_global_load_lds(sp + o, dp + o, 16, 0, 16);
+                    if (o + lane < n16) {
+                    if (a.diag & 2) __builtin_amdgcn_global_load_lds(sp + o, dp + o, 16, 0, 0);
+                    else __builtin_amdgcn_global_load_lds(sp + o, dp + o, 16, 0, 16);
+                }
             }
         }
         sg_sync(sbar, epoch);   // this part's runs are in LDS
