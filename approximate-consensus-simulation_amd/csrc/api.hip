@@ -1101,9 +1101,10 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         }
         if (s->binned && s->clean && !partitioned && !s->f32 && s->B == 1 && !s->n_hub && !s->csr_var &&
             cfg->delay_max == 0) {
-            // persistent rounds; ACSIM_PERSIST=0 keeps the two-kernel round
+            // persistent rounds: opt-in (ACSIM_PERSIST=1) until they beat the
+            // two-kernel round (measured 464 vs 126 µs per cfg4 round, profiles/r03_s1_persist.jsonl)
             const char* pv = getenv("ACSIM_PERSIST");
-            if (!(pv && pv[0] == '0')) {
+            if (pv && pv[0] == '1') {
                 const hipError_t pe = persist_build(s->pers, s->bin, s->N, s->d, cfg->trim, cfg->rule, s->stream);
                 if (pe != hipSuccess && pe != hipErrorNotSupported) CREATE_TRY(pe);
                 if (s->pers.on) {

@@ -18,6 +18,12 @@ from acsim.config import Config, preset
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def persist_on(monkeypatch):
+    """The persistent round is opt-in (ACSIM_PERSIST=1) while it is slower than the two-kernel one."""
+    monkeypatch.setenv("ACSIM_PERSIST", "1")
+
+
 @contextlib.contextmanager
 def env(**kw):
     old = {k: os.environ.get(k) for k in kw}
