@@ -87,6 +87,12 @@ CASES = {
                                                fault_model="crash", n_faulty=600, crash_window=4, loss_p=0.1,
                                                eps=1e-8, max_rounds=300, seed=47, trace_spread=True), 1024),
     "faulty_cfg4_byz_shape_2e17": (preset("cfg4_byz", n_nodes=1 << 17, trace_spread=True), 16384),
+    # 65-128 runs per receiver block in two passes (per-part descriptor sets: the N > 2^20 shape)
+    "runs98_d32_t5_split_sa2048": (Config(n_nodes=200000, topology="regular", degree=32, rule="trimmed", trim=5,
+                                          eps=1e-9, max_rounds=100, seed=48, trace_spread=True), 2048),
+    "faulty_runs79_d32_t5_drop_split_sa2048": (Config(n_nodes=160000, topology="regular", degree=32,
+                                                      rule="trimmed", trim=5, loss_p=0.1, eps=1e-8,
+                                                      max_rounds=200, seed=49, trace_spread=True), 2048),
 }
 
 
@@ -100,6 +106,8 @@ def test_binned_matches_oracle_and_per_lane(oracle_mod, name):
         assert "k_bin_regroup" in kb, kb
     if name.startswith("faulty"):
         assert ",faulty>" in kb, kb
+    if "split" in name:
+        assert " split2" in kb, kb
     with env(ACSIM_BINNED=0):
         kr, rr, xr, tr = run_gpu(cfg)
     assert kr.startswith("k_round_regular"), kr
