@@ -89,8 +89,9 @@ struct acs_sim {
     uint32_t* n_done = nullptr;
     double* trace = nullptr;
     uint32_t* h_ndone = nullptr;   // pinned [2]
-    RunSummary* dsum = nullptr;    // acs_run's summary, folded on the device
-    RunSummary* h_sum = nullptr;   // pinned copy
+    RunSummary* h_sum = nullptr;   // pinned, host-mapped: the one-launch summary writes it directly
+    RunSummary* h_sum_dev = nullptr;   // h_sum's device address
+    void* sum_scratch = nullptr;       // launch_run_summary_mapped's partials and arrival counter
     bool want_summary = false;     // acs_run on a one-launch path: enqueue the summary before the sync
     bool summary_ready = false;    // h_sum holds the summary of the current state
     uint32_t round = 0;            // round of every unfinished instance
@@ -282,7 +283,7 @@ static void release(acs_sim* s) {
     (void)hipFree(s->n_done);
     (void)hipFree(s->trace);
     if (s->h_ndone) (void)hipHostFree(s->h_ndone);
-    (void)hipFree(s->dsum);
+    (void)hipFree(s->sum_scratch);
     if (s->h_sum) (void)hipHostFree(s->h_sum);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
@@ -701,14 +702,18 @@ static int advance(acs_sim* s, uint32_t k) {
         else
             HIP_TRY(launch_batched_small(a, s->B, k, s->stream));
         if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
-        HIP_TRY(hipMemcpyAsync(s->h_ndone, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
-        if (s->want_summary) {   // acs_run: the result summary rides on the same synchronisation
-            HIP_TRY(launch_run_summary(s->st, s->B, s->dsum, s->stream));
-            HIP_TRY(hipMemcpyAsync(s->h_sum, s->dsum, sizeof(RunSummary), hipMemcpyDeviceToHost, s->stream));
+        if (s->want_summary) {
+            // acs_run: the result summary and the done count ride on the same synchronisation, in
+            // one launch that writes host memory (no copies: each costs a DMA round trip, which
+            // bounded the per-rank time of small cfg3 shards)
+            HIP_TRY(launch_run_summary_mapped(s->st, s->B, s->n_done, s->sum_scratch, s->h_sum_dev, s->stream));
             s->summary_ready = true;
+        } else {
+            HIP_TRY(hipMemcpyAsync(s->h_ndone, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
         }
         HIP_TRY(hipStreamSynchronize(s->stream));
         s->round += k;
+        if (s->want_summary) s->h_ndone[0] = s->h_sum->n_done;
         s->all_done = s->h_ndone[0] == s->B;
         return ACS_OK;
     }
@@ -1052,14 +1057,42 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     }
     CREATE_TRY(hipMalloc(&s->n_done, sizeof(uint32_t)));
     CREATE_TRY(hipHostMalloc(&s->h_ndone, 2 * sizeof(uint32_t), hipHostMallocDefault));
-    CREATE_TRY(hipMalloc(&s->dsum, sizeof(RunSummary)));
-    CREATE_TRY(hipHostMalloc(&s->h_sum, sizeof(RunSummary), hipHostMallocDefault));
+    CREATE_TRY(hipHostMalloc(&s->h_sum, sizeof(RunSummary), hipHostMallocMapped));
+    CREATE_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&s->h_sum_dev), s->h_sum, 0));
+    CREATE_TRY(hipMalloc(&s->sum_scratch, kSummaryScratch));
+    CREATE_TRY(hipMemsetAsync(s->sum_scratch, 0, kSummaryScratch, s->stream));
     if (cfg->trace_spread) {
         const uint64_t nt = s->B * ((uint64_t)cfg->max_rounds + 1);
         CREATE_TRY(hipMalloc(&s->trace, nt * sizeof(double)));
         CREATE_TRY(hipMemsetAsync(s->trace, 0xFF, nt * sizeof(double), s->stream));   // NaN
     }
     const bool tagged = cfg->fault_model != ACS_FAULT_NONE;
+    if (cfg->fault_model != ACS_FAULT_NONE) {
+        CREATE_TRY(hipMalloc(&s->status, s->B * s->N * sizeof(uint32_t)));
+        CREATE_TRY(build_fault_status(s->status, s->B, s->N, cfg->n_faulty, cfg->fault_model,
+                                      cfg->crash_window, s->mp.key, cfg->instance_offset, s->stream));
+        if (s->binned && s->f32 && cfg->fault_model == ACS_FAULT_CRASH && s->N > (1ull << 20)) {
+            // crash ranks for the fp32 tags (RoundArgs::crank): faulty nodes grouped by crash round
+            std::vector<uint32_t> st(s->N), rank(s->N, 0u), list;
+            CREATE_TRY(hipMemcpy(st.data(), s->status, s->N * sizeof(uint32_t), hipMemcpyDeviceToHost));
+            const uint32_t W = cfg->crash_window;
+            s->coff.assign(W + 1, 0u);
+            for (uint64_t i = 0; i < s->N; ++i)
+                if (st[i] < W) ++s->coff[st[i] + 1];
+            for (uint32_t w = 0; w < W; ++w) s->coff[w + 1] += s->coff[w];
+            list.resize(s->coff[W] ? s->coff[W] : 1);
+            std::vector<uint32_t> fill(s->coff.begin(), s->coff.end() - 1);
+            for (uint64_t i = 0; i < s->N; ++i)
+                if (st[i] < W) {
+                    rank[i] = fill[st[i]] - s->coff[st[i]];
+                    list[fill[st[i]]++] = (uint32_t)i;
+                }
+            CREATE_TRY(hipMalloc(&s->crank, s->N * sizeof(uint32_t)));
+            CREATE_TRY(hipMalloc(&s->clist, list.size() * sizeof(uint32_t)));
+            CREATE_TRY(hipMemcpy(s->crank, rank.data(), s->N * sizeof(uint32_t), hipMemcpyHostToDevice));
+            CREATE_TRY(hipMemcpy(s->clist, list.data(), list.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        }
+    }
     if (cfg->topology == ACS_TOPO_RANDOM_REGULAR) {
         const uint64_t words = ((rows_local + 63) / 64) * 64ull * s->dp;
         CREATE_TRY(hipMalloc(&s->ell, words * sizeof(uint32_t)));
@@ -1072,7 +1105,8 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         bool bin_refused = false;
         auto try_plan = [&](BinnedPlan& plan, const uint32_t* ell, uint64_t nr) -> hipError_t {
             if (!s->binned || bin_refused || !nr) return hipSuccess;
-            hipError_t e = binned_build(plan, ell, s->N, nr, s->d, s->dp, bin_sa, tagged, s->f32, bin_of, s->stream);
+            hipError_t e = binned_build(plan, ell, s->N, nr, s->d, s->dp, bin_sa, tagged, s->f32, bin_of, s->stream,
+                                        false, s->status);
             if (e == hipErrorNotSupported) {
                 bin_refused = true;
                 return hipSuccess;
@@ -1120,38 +1154,16 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
             // NP-pass phase B (slot-dependent configs: fp64, two passes only; see launch_round_binned)
             if (!s->pers.on && s->bin.split > 1 && (s->clean || (!s->f32 && s->bin.split == 2)))
                 s->kname += " split" + std::to_string(s->bin.split);
+            if (s->bin.fix) {   // fault fix-up list instead of tagged senders
+                const size_t pos = s->kname.find("+k_bin_tag");
+                if (pos != std::string::npos) s->kname.replace(pos, 10, "+k_bin_fixup");
+            }
             (void)hipFree(s->ell);
             s->ell = nullptr;
             for (Part& q : s->parts) {
                 (void)hipFree(q.ell);
                 q.ell = nullptr;
             }
-        }
-    }
-    if (cfg->fault_model != ACS_FAULT_NONE) {
-        CREATE_TRY(hipMalloc(&s->status, s->B * s->N * sizeof(uint32_t)));
-        CREATE_TRY(build_fault_status(s->status, s->B, s->N, cfg->n_faulty, cfg->fault_model,
-                                      cfg->crash_window, s->mp.key, cfg->instance_offset, s->stream));
-        if (s->binned && s->f32 && cfg->fault_model == ACS_FAULT_CRASH && s->N > (1ull << 20)) {
-            // crash ranks for the fp32 tags (RoundArgs::crank): faulty nodes grouped by crash round
-            std::vector<uint32_t> st(s->N), rank(s->N, 0u), list;
-            CREATE_TRY(hipMemcpy(st.data(), s->status, s->N * sizeof(uint32_t), hipMemcpyDeviceToHost));
-            const uint32_t W = cfg->crash_window;
-            s->coff.assign(W + 1, 0u);
-            for (uint64_t i = 0; i < s->N; ++i)
-                if (st[i] < W) ++s->coff[st[i] + 1];
-            for (uint32_t w = 0; w < W; ++w) s->coff[w + 1] += s->coff[w];
-            list.resize(s->coff[W] ? s->coff[W] : 1);
-            std::vector<uint32_t> fill(s->coff.begin(), s->coff.end() - 1);
-            for (uint64_t i = 0; i < s->N; ++i)
-                if (st[i] < W) {
-                    rank[i] = fill[st[i]] - s->coff[st[i]];
-                    list[fill[st[i]]++] = (uint32_t)i;
-                }
-            CREATE_TRY(hipMalloc(&s->crank, s->N * sizeof(uint32_t)));
-            CREATE_TRY(hipMalloc(&s->clist, list.size() * sizeof(uint32_t)));
-            CREATE_TRY(hipMemcpy(s->crank, rank.data(), s->N * sizeof(uint32_t), hipMemcpyHostToDevice));
-            CREATE_TRY(hipMemcpy(s->clist, list.data(), list.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
         }
     }
     if (cfg->topology == ACS_TOPO_CSR) {
@@ -1169,7 +1181,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
             if (s->ell_sorted) CREATE_TRY(launch_sort_ell_rows(s->ell, s->N, s->d, s->stream));
             if (s->binned) {
                 const hipError_t be = binned_build(s->bin, s->ell, s->N, s->N, s->d, s->dp, bin_sa, tagged, s->f32, false,
-                                                   s->stream, true);
+                                                   s->stream, true, s->status);
                 if (be == hipErrorNotSupported) {   // the plan does not fit: the per-lane kernel serves the rows
                     binned_free(s->bin);
                     s->binned = false;
@@ -1382,8 +1394,7 @@ int acs_run(acs_sim* s, acs_result* out) {
     const auto t1 = std::chrono::steady_clock::now();
     if (out) {   // the summary is folded on the device: 32 bytes back instead of B states
         if (!s->summary_ready) {
-            HIP_TRY(launch_run_summary(s->st, s->B, s->dsum, s->stream));
-            HIP_TRY(hipMemcpyAsync(s->h_sum, s->dsum, sizeof(RunSummary), hipMemcpyDeviceToHost, s->stream));
+            HIP_TRY(launch_run_summary_mapped(s->st, s->B, nullptr, s->sum_scratch, s->h_sum_dev, s->stream));
             HIP_TRY(hipStreamSynchronize(s->stream));
         }
         s->summary_ready = false;

@@ -128,10 +128,15 @@ hipError_t launch_partials_from_x(const double* x, const uint32_t* status, uint6
                                   double2* partial, uint32_t nblk, bool f32, hipStream_t s);
 hipError_t launch_finalize(const FinalizeArgs& a, uint64_t B, hipStream_t s);
 struct RunSummary {   // acs_run's result, folded on the device (32 bytes)
-    unsigned int rounds_max, pad;
+    unsigned int rounds_max, n_done;   // (n_done: written by the one-launch form only)
     unsigned long long n_converged, rounds_sum, spread_max_bits;
 };
-hipError_t launch_run_summary(const InstState* st, uint64_t B, RunSummary* out, hipStream_t s);
+// acs_run's summary in ONE launch with no copy: block partials, then the last block to arrive folds
+// them and stores the summary (and *n_done) straight into host-mapped memory `out`.  scratch: a
+// device buffer of kSummaryScratch bytes whose first word is zero (the last block re-zeroes it).
+constexpr uint32_t kSummaryScratch = 1024 * 32 + 64;
+hipError_t launch_run_summary_mapped(const InstState* st, uint64_t B, const uint32_t* n_done, void* scratch,
+                                     RunSummary* out, hipStream_t s);
 
 // ---- round kernels
 // Register-resident kernel for RANDOM_REGULAR with a compiled (d, t) pair; returns
@@ -176,6 +181,10 @@ struct BinnedPlan {
     double* xtag = nullptr;             // [N+2] tagged sender values (fault schedules only)
     uint64_t* ts = nullptr;             // ACSIM_BIN_TS=<file>: [3 * (ts_a + ts_b)] workgroup timestamps of the last round
     uint32_t ts_a = 0, ts_b = 0;        // phase-A / phase-B workgroups recorded
+    // fault fix-up: fix[k] = (last-stage position, local row, slot, sender) of every
+    // delivery from a sender that is not honest; nullptr: tagged senders (k_bin_tag) instead
+    uint4* fix = nullptr;
+    uint32_t nfix = 0;
 };
 bool binned_supported(uint32_t d, uint32_t t, uint32_t rule);
 // 1 or 2 exchange levels for NR local receivers of an N-node graph (0: not supported).
@@ -184,7 +193,8 @@ uint32_t binned_levels(uint64_t N, uint64_t NR, uint32_t d, uint32_t sa, uint32_
 // need spec order); sa = source block size; tagged: the config has a fault schedule; ofree: clean
 // config under a sort-based rule (order-free phase B: rid instead of invpos).
 hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t NR, uint32_t d, uint32_t dp,
-                        uint32_t sa, bool tagged, bool f32, bool ofree, hipStream_t s, bool var = false);
+                        uint32_t sa, bool tagged, bool f32, bool ofree, hipStream_t s, bool var = false,
+                        const uint32_t* status = nullptr);
 void binned_free(BinnedPlan& p);
 // clean: no slot-dependent decision (selects the plain phase-B instantiation)
 // fin: the previous round's finalize, deferred into this round's phase A (nullptr: none pending)

@@ -40,8 +40,19 @@ __global__ __launch_bounds__(kReduceBlock) void k_finalize(const FinalizeArgs a)
 // acs_run's summary over the B instance states (rounds_max, converged count, Σ rounds, max final
 // spread) folded on the device, so a run returns 32 bytes instead of copying B states to the host.
 // Spreads are >= +0.0, so their bit patterns order as unsigned integers.
-__global__ __launch_bounds__(kReduceBlock) void k_run_summary(const InstState* __restrict__ st, uint64_t B,
-                                                              RunSummary* out) {
+// One-launch summary (launch_run_summary_mapped): per-block partial -> agent-scope release ->
+// arrival counter; the last block acquires, folds the partials and writes `out` (host memory).
+struct SumPart {
+    uint32_t rmax, conv;
+    uint64_t rsum, smax;
+};
+__global__ __launch_bounds__(kReduceBlock) void k_run_summary_mapped(const InstState* __restrict__ st, uint64_t B,
+                                                                     const uint32_t* __restrict__ n_done,
+                                                                     unsigned char* scratch, RunSummary* out) {
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(scratch);
+    SumPart* part = reinterpret_cast<SumPart*>(scratch + 64);
+    __shared__ SumPart red[kReduceBlock / 64];
+    __shared__ uint32_t last;
     uint32_t rmax = 0, conv = 0;
     uint64_t rsum = 0, smax = 0;
     for (uint64_t b = (uint64_t)blockIdx.x * kReduceBlock + threadIdx.x; b < B; b += (uint64_t)gridDim.x * kReduceBlock) {
@@ -52,28 +63,67 @@ __global__ __launch_bounds__(kReduceBlock) void k_run_summary(const InstState* _
         const uint64_t sb = (uint64_t)__double_as_longlong(e.spread);
         smax = sb > smax ? sb : smax;
     }
+    auto fold_wave = [&]() {
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        const uint32_t r2 = __shfl_xor(rmax, o, 64);
-        const uint64_t s2 = __shfl_xor(smax, o, 64);
-        rmax = r2 > rmax ? r2 : rmax;
-        smax = s2 > smax ? s2 : smax;
-        conv += __shfl_xor(conv, o, 64);
-        rsum += __shfl_xor(rsum, o, 64);
+        for (int o = 32; o >= 1; o >>= 1) {
+            const uint32_t r2 = __shfl_xor(rmax, o, 64);
+            const uint64_t s2 = __shfl_xor(smax, o, 64);
+            rmax = r2 > rmax ? r2 : rmax;
+            smax = s2 > smax ? s2 : smax;
+            conv += __shfl_xor(conv, o, 64);
+            rsum += __shfl_xor(rsum, o, 64);
+        }
+    };
+    auto fold_block = [&]() {   // -> thread 0
+        fold_wave();
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = SumPart{rmax, conv, rsum, smax};
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (uint32_t w = 1; w < kReduceBlock / 64; ++w) {
+                rmax = red[w].rmax > rmax ? red[w].rmax : rmax;
+                smax = red[w].smax > smax ? red[w].smax : smax;
+                conv += red[w].conv;
+                rsum += red[w].rsum;
+            }
+    };
+    fold_block();
+    if (threadIdx.x == 0) {
+        part[blockIdx.x] = SumPart{rmax, conv, rsum, smax};
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == gridDim.x;
     }
-    if ((threadIdx.x & 63) == 0) {
-        atomicMax(&out->rounds_max, rmax);
-        atomicAdd(&out->n_converged, (unsigned long long)conv);
-        atomicAdd(&out->rounds_sum, (unsigned long long)rsum);
-        atomicMax(&out->spread_max_bits, (unsigned long long)smax);
+    __syncthreads();
+    if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    rmax = 0, conv = 0, rsum = 0, smax = 0;
+    for (uint32_t k = threadIdx.x; k < gridDim.x; k += kReduceBlock) {
+        const SumPart q = part[k];
+        rmax = q.rmax > rmax ? q.rmax : rmax;
+        smax = q.smax > smax ? q.smax : smax;
+        conv += q.conv;
+        rsum += q.rsum;
+    }
+    __syncthreads();   // (red[] reuse)
+    fold_block();
+    if (threadIdx.x == 0) {
+        out->rounds_max = rmax;
+        out->n_done = n_done ? *n_done : 0u;
+        out->n_converged = conv;
+        out->rounds_sum = rsum;
+        out->spread_max_bits = smax;
+        *cnt = 0;   // ready for the next launch (stream-ordered)
     }
 }
 
-hipError_t launch_run_summary(const InstState* st, uint64_t B, RunSummary* out, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(out, 0, sizeof(RunSummary), s);
-    if (e != hipSuccess) return e;
+hipError_t launch_run_summary_mapped(const InstState* st, uint64_t B, const uint32_t* n_done, void* scratch,
+                                     RunSummary* out, hipStream_t s) {
     const uint64_t g = (B + kReduceBlock - 1) / kReduceBlock;
-    hipLaunchKernelGGL(k_run_summary, dim3((unsigned)(g < 1024 ? g : 1024)), dim3(kReduceBlock), 0, s, st, B, out);
+    static_assert(64 + 1024 * sizeof(SumPart) <= kSummaryScratch, "summary scratch");
+    hipLaunchKernelGGL(k_run_summary_mapped, dim3((unsigned)(g == 0 ? 1 : g < 1024 ? g : 1024)), dim3(kReduceBlock), 0, s,
+                       st, B, n_done, reinterpret_cast<unsigned char*>(scratch), out);
     return hipGetLastError();
 }
 

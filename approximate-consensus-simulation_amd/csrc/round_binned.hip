@@ -158,6 +158,32 @@ __global__ __launch_bounds__(256) void k_bin_tag(const VT* __restrict__ x, const
     }
 }
 
+// Fault fix-up: fix[k] = (stage position, local receiver row, slot t, sender j) for
+// every delivery from a sender that is not honest.  Each round it writes the §A.4 / §A.6 resolution
+// of that delivery into the last stage (Byzantine value, x_j, or a quiet NaN for a missing
+// message); drops are phase B's.  The stream of phase A carried plain x there.
+template <typename VT = double>
+__global__ __launch_bounds__(256) void k_bin_fixup(const uint4* __restrict__ fix, uint32_t nfix, const RoundArgs a,
+                                                   VT* __restrict__ stage, uint32_t D) {
+    const InstState* S = a.st;
+    if (S->done) return;
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= nfix) return;
+    const uint4 f = fix[k];
+    const uint64_t i = a.row0 + f.y;
+    const uint32_t stj = a.status[f.w];
+    const uint64_t slot = a.rowptr ? a.rowptr[i] + f.z : i * D + f.z;
+    const VT xj = reinterpret_cast<const VT*>(a.xin)[f.w];
+    bool miss;
+    const VT v = resolve_entry_m(a.mp, stj, xj, xj, false, (uint32_t)a.mp.inst_offset, a.r, (uint32_t)i, slot,
+                                 (VT)S->lo, (VT)S->hi, miss);
+    if constexpr (sizeof(VT) == 8)
+        stage[f.x] = miss ? __longlong_as_double((long long)(kTagBase | 3u)) : v;
+    else
+        stage[f.x] = miss ? __uint_as_float(kTagBase32 | 3u) : v;
+}
+
+
 // VAR: a CSR graph padded to D (§8(f) row 1): slots t >= deg(i) are absent entries, slot numbers
 // are rowptr[i] + t (one drop draw each); single pass only.
 // Faulty NP > 1: the parts' LDS buffers admit 4 workgroups per CU, but the faulty bodies need more
@@ -170,12 +196,19 @@ __global__ __launch_bounds__(256) void k_bin_tag(const VT* __restrict__ x, const
 #else
 #define ACS_FAULTY_WPE_OF(T, W) ((T) == 5 && !(W) ? 3 : 2)
 #endif
-template <int D, int T, bool WMSR = false, bool FAULTY = false, typename VT = double, int NP = 1, bool VAR = false>
-__global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) : 1) void k_bin_gather(const RoundArgs a, const VT* __restrict__ stage,
+// FIX (fault fix-up plans): the stage already holds every faulty sender's resolved
+// delivery (k_bin_fixup), a missing one as a quiet NaN; phase B draws the §A.5 drop mask, turns
+// dropped and NaN entries into missing ones and applies the receiver's own status — no tag
+// decoding, no Byzantine draws, clean-kernel registers.
+template <int D, int T, bool WMSR = false, bool FAULTY = false, typename VT = double, int NP = 1, bool VAR = false,
+          bool FIX = false>
+__global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) : FIX && NP > 1 && (T || WMSR) ? 4 : 1) void k_bin_gather(const RoundArgs a, const VT* __restrict__ stage,
                                                        const uint16_t* __restrict__ invpos,
                                                        const uint2* __restrict__ tiles, uint32_t nrun, uint32_t Q,
                                                        uint32_t Qc, uint32_t pol) {
     static_assert(D % 8 == 0, "invpos is read 8 slots at a time");
+    static_assert(!(FIX && FAULTY), "FIX replaces the tagged resolution");
+    constexpr bool FLT = FAULTY || FIX;   // a fault schedule or loss: receiver status and drop mask
     // runs are padded to 16-byte multiples; nrun <= D*kBinSB/16 (checked when the plan is built)
     __shared__ __attribute__((aligned(16)))
     VT raw[NP > 1 ? kBinPartCap<D, NP> : D * kBinSB + D * kBinSB / 16 * (16 / sizeof(VT) - 1)];
@@ -218,7 +251,7 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
     // ordinary loads next (their wait is the barrier's vmcnt(0) anyway)
     const VT xi = live ? reinterpret_cast<const VT*>(a.xin)[i] : VT(0);
     uint32_t si = kHonest;
-    if constexpr (FAULTY) {
+    if constexpr (FLT) {
         if (a.status && live) si = a.status[i];
     }
     uint32_t dg = D;
@@ -226,7 +259,7 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
     if constexpr (VAR) {
         if (live) {
             dg = a.deg[i];
-            if constexpr (FAULTY) rp = a.rowptr[i];
+            if constexpr (FLT) rp = a.rowptr[i];
         }
     }
     // §A.5 drop decisions of the lane's D slots as a bit mask, drawn before the values arrive: the
@@ -234,7 +267,7 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
     // below, the faulty two-pass kernels spilled 36-49 VGPRs at their 128-VGPR bound, and the CSR
     // slot loop — one draw per slot — was too large to unroll, so v[] went to scratch)
     uint32_t dmask = 0;
-    if constexpr (FAULTY) {
+    if constexpr (FLT) {
         static_assert(D <= 32, "one drop bit per slot in a 32-bit mask");
         const MsgParams& mp = a.mp;
         if (mp.thr && live) {
@@ -339,10 +372,10 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
     double mn = kInf, mx = -kInf;
     if (live) {
         VT res = xi;
-        if (!FAULTY || is_active(si, a.r)) {
+        if (!FLT || is_active(si, a.r)) {
             v[0] = xi;
             uint32_t nmiss = 0;   // entries left out under missing_policy = OMIT
-            if constexpr (VAR && !FAULTY) {   // absent CSR entries
+            if constexpr (VAR && !FAULTY && !FIX) {   // absent CSR entries
 #pragma unroll
                 for (int t = 0; t < D; ++t)
                     if ((uint32_t)t >= dg) {
@@ -393,6 +426,19 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
                         v[1 + t] = out ? omit_fill<VT>(a.rule) : rv;
                         nmiss += out;
                     }
+                }
+            }
+            if constexpr (FIX) {   // drops and the fix-up's missing entries (NaN) -> x_i (missing_policy
+                                   // = SUBSTITUTE: OMIT configs keep the tagged path); absent CSR entries
+#pragma unroll
+                for (int t = 0; t < D; ++t) {
+                    if (VAR && (uint32_t)t >= dg) {
+                        v[1 + t] = omit_fill<VT>(a.rule);
+                        ++nmiss;
+                        continue;
+                    }
+                    const VT u = v[1 + t];
+                    v[1 + t] = (((dmask >> t) & 1u) || u != u) ? xi : u;
                 }
             }
             if (VAR || (FAULTY && a.mp.omit))
@@ -757,6 +803,26 @@ __global__ __launch_bounds__(256) void k_bin_rid(uint64_t E, BinGeom G, uint32_t
     rid[(uint64_t)b * rstride + pos] = (uint8_t)(li % kBinSB);
 }
 
+// fix-up list: every sorted position p of the last level whose sender is not honest
+__global__ __launch_bounds__(256) void k_bin_fixlist(const uint32_t* __restrict__ ell, uint64_t E, uint32_t D,
+                                                     uint32_t dp, uint32_t none, const uint32_t* __restrict__ ks,
+                                                     const uint32_t* __restrict__ vs, const uint2* __restrict__ tl,
+                                                     const uint32_t* __restrict__ pstart,
+                                                     const uint32_t* __restrict__ status,
+                                                     uint4* __restrict__ fix, uint32_t cap, uint32_t* __restrict__ cnt) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= E) return;
+    const uint32_t key = ks[p];
+    if (key >= none) return;
+    const uint32_t e = vs[p];
+    const uint64_t li = e / D;
+    const uint32_t t = e % D;
+    const uint32_t j = ell_at(ell, li, t, dp);
+    if (status[j] == kHonest) return;
+    const uint32_t k = atomicAdd(cnt, 1u);
+    if (k < cap) fix[k] = make_uint4(pstart[key] + (uint32_t)(p - tl[key].x), (uint32_t)li, t, j);
+}
+
 // ------------------------------------------------------------------------------ host side
 #define ACS_BINNED_VARIANTS(X) X(16, 5) X(32, 5) X(16, 0) X(32, 0) X(8, 2) X(8, 0)
 
@@ -813,6 +879,7 @@ void binned_free(BinnedPlan& p) {
     (void)hipFree(p.stage1);
     (void)hipFree(p.stage2);
     (void)hipFree(p.xtag);
+    (void)hipFree(p.fix);
     p = BinnedPlan{};
 }
 
@@ -883,7 +950,8 @@ hipError_t tile_sort(const uint32_t* ell, uint64_t E, const BinGeom& G, int leve
 }  // namespace
 
 hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t NR, uint32_t d, uint32_t dp,
-                        uint32_t sa, bool tagged, bool f32, bool ofree, hipStream_t s, bool var) {
+                        uint32_t sa, bool tagged, bool f32, bool ofree, hipStream_t s, bool var,
+                        const uint32_t* status) {
     if (var && (f32 || ofree)) return hipErrorNotSupported;   // CSR plans: fp64, invpos phase B
     hipError_t e = hipSuccess;
     uint32_t sr = 0;
@@ -1015,6 +1083,31 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
             e = hipGetLastError();
         }
     }
+    // fault fix-up list: when the faulty senders' deliveries are few (at most an
+    // eighth of all), their resolutions are written into the stage instead of tagging every sender
+    if (e == hipSuccess && tagged && status && !ofree) {
+        const uint32_t cap = (uint32_t)(E / 8 + 1);
+        uint32_t* cnt = nullptr;
+        e = hipMalloc(&p.fix, (uint64_t)cap * sizeof(uint4));
+        if (e == hipSuccess) e = hipMalloc(&cnt, sizeof(uint32_t));
+        if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, sizeof(uint32_t), s);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_bin_fixlist, dim3(grid), dim3(256), 0, s, ell, E, G.D, G.dp,
+                               levels == 1 ? G.none1 : G.none2, last->ks, last->vs, last->tl, last->pstart, status,
+                               p.fix, cap, cnt);
+            e = hipGetLastError();
+        }
+        uint32_t n = 0;
+        if (e == hipSuccess) e = hipMemcpyAsync(&n, cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        (void)hipFree(cnt);
+        if (e == hipSuccess && n <= cap && !getenv("ACSIM_BIN_NOFIX")) {
+            p.nfix = n;
+        } else {
+            (void)hipFree(p.fix);
+            p.fix = nullptr;
+        }
+    }
     hipError_t e2 = hipStreamSynchronize(s);
     if (e == hipSuccess) e = e2;
     // NP-pass phase B: 2 passes by default where the whole image limits phase B to 2 workgroups
@@ -1136,10 +1229,12 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
     const uint32_t nslot_all = a.nblk > p.Q ? a.nblk : p.Q;
     if (a.qhi > nslot_all) a.qhi = nslot_all;
     if (a.qlo >= a.qhi) phases &= ~4u;
+    // fault fix-up on whole rounds; chunked partitioned rounds keep the tagged senders
+    const bool fixp = !clean && a.status && p.fix && phases == 7 && sel.n == 0 && !a.mp.omit;
     if (p.f32) {   // fp32 plans: one or two levels; tagged senders need N <= 2^20
         float* st1 = reinterpret_cast<float*>(p.stage1);
         const float* fsrc = reinterpret_cast<const float*>(a.xin);
-        if (!clean && a.status) {
+        if (!clean && a.status && !fixp) {
             // the 20-bit id field holds a sender id up to 2^20 nodes, beyond that a crash rank
             if (!p.xtag || (a.N > (1ull << 20) && a.mp.fault == 1 && !a.crank)) return hipErrorInvalidValue;
             float* xt = reinterpret_cast<float*>(p.xtag);
@@ -1158,6 +1253,8 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
                                    p.mt, p.moff, p.idxM, st2, a.st, p.PK, pol);
             st1 = st2;   // phase B reads the regrouped stage
         }
+        if (fixp)
+            hipLaunchKernelGGL(k_bin_fixup<float>, dim3((p.nfix + 255) / 256), dim3(256), 0, s, p.fix, p.nfix, a, st1, p.D);
         if (!(phases & 4)) return hipGetLastError();
         const uint32_t Qc = (a.qhi - a.qlo + 7) / 8;
         const dim3 grid(8 * Qc);
@@ -1169,6 +1266,12 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
         else if (p.ofree)                                                                                \
             hipLaunchKernelGGL((k_bin_gather_of<DD, TT, false, float>), grid, dim3(kBinSB), 0, s, a, st1,   \
                                p.rid, p.rstride, p.tiles, p.nrun, p.Q, Qc);                              \
+        else if (fixp && a.rule == 4)                                                                    \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, true, false, float, 1, false, true>), grid, dim3(kBinSB), 0, \
+                               s, a, st1, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                           \
+        else if (fixp)                                                                                   \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, false, false, float, 1, false, true>), grid, dim3(kBinSB), 0, \
+                               s, a, st1, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                           \
         else if (!clean && a.rule == 4)                                                                  \
             hipLaunchKernelGGL((k_bin_gather<DD, TT, true, true, float>), grid, dim3(kBinSB), 0, s, a, st1,  \
                                p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                      \
@@ -1192,7 +1295,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
         return hipErrorNotSupported;
     }
     const double* src = a.xin;
-    if (!clean && a.status) {
+    if (!clean && a.status && !fixp) {
         if (!p.xtag) return hipErrorInvalidValue;
         if (phases & 1)
             hipLaunchKernelGGL(k_bin_tag<double>, dim3((unsigned)((a.N + 511) / 512)), dim3(256), 0, s, a.xin, a.status,
@@ -1212,6 +1315,9 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
         if ((e = hipGetLastError()) != hipSuccess) return e;
         last = p.stage2;
     }
+    if (fixp)
+        hipLaunchKernelGGL(k_bin_fixup<double>, dim3((p.nfix + 255) / 256), dim3(256), 0, s, p.fix, p.nfix, a,
+                           const_cast<double*>(last), p.D);
     if (!(phases & 4)) return hipGetLastError();
     const uint32_t Qc = (a.qhi - a.qlo + 7) / 8;
     const dim3 grid(8 * Qc);
@@ -1224,6 +1330,24 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
         else if (p.var && clean)                                                                         \
             hipLaunchKernelGGL((k_bin_gather<DD, TT, false, false, double, 1, true>), grid, dim3(kBinSB), 0, s, \
                                a, last, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                             \
+        else if (fixp && p.var && w_)                                                                    \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, true, false, double, 1, true, true>), grid, dim3(kBinSB), 0, \
+                               s, a, last, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                          \
+        else if (fixp && p.var)                                                                          \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, false, false, double, 1, true, true>), grid, dim3(kBinSB), 0, \
+                               s, a, last, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                          \
+        else if (fixp && p.split == 2 && w_)                                                             \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, true, false, double, 2, false, true>), grid, dim3(kBinSB), 0, \
+                               s, a, last, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                          \
+        else if (fixp && p.split == 2)                                                                   \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, false, false, double, 2, false, true>), grid, dim3(kBinSB), 0, \
+                               s, a, last, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                          \
+        else if (fixp && w_)                                                                             \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, true, false, double, 1, false, true>), grid, dim3(kBinSB), 0, \
+                               s, a, last, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                          \
+        else if (fixp)                                                                                   \
+            hipLaunchKernelGGL((k_bin_gather<DD, TT, false, false, double, 1, false, true>), grid, dim3(kBinSB), 0, \
+                               s, a, last, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                          \
         else if (p.var && w_)                                                                            \
             hipLaunchKernelGGL((k_bin_gather<DD, TT, true, true, double, 1, true>), grid, dim3(kBinSB), 0, s, \
                                a, last, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                             \

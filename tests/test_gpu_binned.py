@@ -120,6 +120,28 @@ def test_binned_matches_oracle_and_per_lane(oracle_mod, name):
     assert np.array_equal(tb, to) and np.array_equal(tr, to)
 
 
+@pytest.mark.parametrize("name", [n for n in CASES if n.startswith("faulty")])
+def test_faulty_fixup_and_tagged_paths_match_oracle(oracle_mod, name):
+    """Fault schedules run on the fix-up list by default (k_bin_fixup: the faulty senders'
+    deliveries resolved into the stage) and on tagged senders (k_bin_tag) with
+    ACSIM_BIN_NOFIX=1 or under OMIT; both bit-exact against the oracle."""
+    cfg, sa = CASES[name]
+    with env(ACSIM_BIN_SA=sa):
+        kf, rf, xf, tf = run_gpu(cfg)
+    with env(ACSIM_BIN_SA=sa, ACSIM_BIN_NOFIX=1):
+        kt, rt, xt, tt = run_gpu(cfg)
+    if cfg.fault_model != "none":
+        assert "k_bin_fixup" in kf, kf
+        assert "k_bin_tag" in kt, kt
+    with oracle_mod.OracleSimulator(cfg, threads=8) as o:
+        o.run()
+        ro, xo, to = o.rounds(), bits(o.values(0)), bits(o.spread_trace(0))
+    for r_, x_, t_ in ((rf, xf, tf), (rt, xt, tt)):
+        assert np.array_equal(r_, ro)
+        assert np.array_equal(x_, xo)
+        assert np.array_equal(t_, to)
+
+
 def test_binned_full_cfg4_fixed_matches_per_lane():
     """Full-size headline graph (N = 2^20): 30 FIXED rounds, binned vs per-lane bit for bit."""
     cfg = preset("cfg4", max_rounds=30, trace_spread=True)
@@ -186,10 +208,14 @@ def test_faulty_full_cfg4_byz_matches_per_lane():
     """Full-size cfg4_byz (N = 2^20, 1048 Byzantine RANDOM senders): binned vs per-lane bit for bit."""
     cfg = preset("cfg4_byz", max_rounds=25, trace_spread=True)
     kb, rb, xb, tb = run_gpu(cfg)
-    assert kb.startswith("k_bin_scatter") and "+k_bin_tag" in kb, kb
+    assert kb.startswith("k_bin_scatter") and "+k_bin_fixup" in kb, kb
+    with env(ACSIM_BIN_NOFIX=1):   # the tagged-sender path
+        kt, rt, xt, tt = run_gpu(cfg)
+    assert "+k_bin_tag" in kt, kt
     with env(ACSIM_BINNED=0):
         _, rr, xr, tr = run_gpu(cfg)
     assert np.array_equal(rb, rr) and np.array_equal(xb, xr) and np.array_equal(tb, tr)
+    assert np.array_equal(rt, rr) and np.array_equal(xt, xr) and np.array_equal(tt, tr)
 
 
 def test_faulty_chunks_resume_and_partitions(oracle_mod):

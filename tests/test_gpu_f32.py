@@ -79,7 +79,7 @@ def test_f32_matches_oracle(oracle_mod, name):
 def test_f32_small_complete_graphs_take_the_batched_kernel():
     for name in ("cfg1_f32", "cfg1_avg_f32", "cfg3_slice_f32", "complete_avg_batched"):
         with acsim.Simulator(CASES[name], device=0) as g:
-            assert g.kernel_name().startswith("k_batched_small<"), (name, g.kernel_name())
+            assert g.kernel_name().startswith(("k_batched_small<", "k_batched_split<")), (name, g.kernel_name())
             assert g.kernel_name().endswith("[f32]")
 
 
