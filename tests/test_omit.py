@@ -148,7 +148,8 @@ GPU_CASES = [
 def test_omit_gpu_matches_oracle(oracle_mod, name, envs, kernel):
     cfg = CASES[name]
     kname, r, x, tr = gpu_run(cfg, **envs)
-    assert kname.startswith(kernel), kname
+    # (clean 64-node AVERAGE batches take the split form of the batched kernel)
+    assert kname.startswith(kernel) or (kernel == "k_batched_small" and kname.startswith("k_batched_split")), kname
     with oracle_mod.OracleSimulator(cfg, threads=8) as o:
         o.run()
         assert np.array_equal(o.rounds(), r)
