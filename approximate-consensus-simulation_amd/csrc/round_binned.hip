@@ -1085,25 +1085,29 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     }
     // fault fix-up list: when the faulty senders' deliveries are few (at most an
     // eighth of all), their resolutions are written into the stage instead of tagging every sender
-    if (e == hipSuccess && tagged && status && !ofree) {
-        const uint32_t cap = (uint32_t)(E / 8 + 1);
+    if (e == hipSuccess && tagged && status && !ofree && !getenv("ACSIM_BIN_NOFIX")) {
+        // two passes: count (cap 0), then fill a list of exactly that size
         uint32_t* cnt = nullptr;
-        e = hipMalloc(&p.fix, (uint64_t)cap * sizeof(uint4));
-        if (e == hipSuccess) e = hipMalloc(&cnt, sizeof(uint32_t));
-        if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, sizeof(uint32_t), s);
-        if (e == hipSuccess) {
-            hipLaunchKernelGGL(k_bin_fixlist, dim3(grid), dim3(256), 0, s, ell, E, G.D, G.dp,
-                               levels == 1 ? G.none1 : G.none2, last->ks, last->vs, last->tl, last->pstart, status,
-                               p.fix, cap, cnt);
-            e = hipGetLastError();
-        }
         uint32_t n = 0;
-        if (e == hipSuccess) e = hipMemcpyAsync(&n, cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        e = hipMalloc(&cnt, sizeof(uint32_t));
+        for (int pass = 0; pass < 2 && e == hipSuccess; ++pass) {
+            if (pass == 1 && (n == 0 || (uint64_t)n > E / 8)) break;   // none, or too many to list
+            if (pass == 1) e = hipMalloc(&p.fix, (uint64_t)n * sizeof(uint4));
+            if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, sizeof(uint32_t), s);
+            if (e == hipSuccess) {
+                hipLaunchKernelGGL(k_bin_fixlist, dim3(grid), dim3(256), 0, s, ell, E, G.D, G.dp,
+                                   levels == 1 ? G.none1 : G.none2, last->ks, last->vs, last->tl, last->pstart,
+                                   status, p.fix, pass ? n : 0u, cnt);
+                e = hipGetLastError();
+            }
+            uint32_t c = 0;
+            if (e == hipSuccess) e = hipMemcpyAsync(&c, cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (pass == 0) n = c;
+            else if (e == hipSuccess && c == n) p.nfix = n;
+        }
         (void)hipFree(cnt);
-        if (e == hipSuccess && n <= cap && !getenv("ACSIM_BIN_NOFIX")) {
-            p.nfix = n;
-        } else {
+        if (!p.nfix) {
             (void)hipFree(p.fix);
             p.fix = nullptr;
         }
