@@ -1057,7 +1057,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     }
     CREATE_TRY(hipMalloc(&s->n_done, sizeof(uint32_t)));
     CREATE_TRY(hipHostMalloc(&s->h_ndone, 2 * sizeof(uint32_t), hipHostMallocDefault));
-    CREATE_TRY(hipHostMalloc(&s->h_sum, sizeof(RunSummary), hipHostMallocMapped));
+    CREATE_TRY(hipHostMalloc(&s->h_sum, sizeof(RunSummary), hipHostMallocMapped | hipHostMallocPortable));
     CREATE_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&s->h_sum_dev), s->h_sum, 0));
     CREATE_TRY(hipMalloc(&s->sum_scratch, kSummaryScratch));
     CREATE_TRY(hipMemsetAsync(s->sum_scratch, 0, kSummaryScratch, s->stream));
