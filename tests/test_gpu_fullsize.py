@@ -42,6 +42,12 @@ def run_oracle(oracle_mod, cfg):
     ("cfg4_eps", dict()),                      # ε-terminated
     ("cfg4_byz", dict()),                      # 0.1 % Byzantine RANDOM senders
     ("cfg4", dict(max_rounds=40, dtype="f32")),
+    # fault fix-up at full size: 1 % crash faults (partial crash draws over 6
+    # rounds) with 5 % loss; Byzantine SPLIT with Δ; fp32 RANDOM Byzantine
+    ("cfg4_eps", dict(fault_model="crash", n_faulty=10486, crash_window=6, loss_p=0.05, max_rounds=60)),
+    ("cfg4_eps", dict(fault_model="byzantine", n_faulty=3000, byz_strategy="split", byz_delta=0.01,
+                      max_rounds=60)),
+    ("cfg4_byz", dict(dtype="f32", max_rounds=60)),
 ])
 def test_cfg4_full_size_bit_exact(oracle_mod, name, over):
     cfg = preset(name, trace_spread=True, **over)
