@@ -138,14 +138,11 @@ struct acs_sim {
     double* dsorted = nullptr;     // dense path: sorted base multiset [N]
     uint32_t* dcounts = nullptr;   // dense path: |B|, #Byzantine, #crash-silent
     std::vector<Part> parts;       // virtual partitions 1..P-1 (partition 0 uses x / ell)
-    // persistent binned rounds (round_persist.hip): one launch per round(k) call
-    PersistPlan pers;
-    uint64_t pers_abort = 0;
     // kernel timing (bench)
     uint32_t timing = 0;           // 0 off, else bracket every timing-th round (sampling)
     uint64_t timing_ctr = 0;
     std::vector<hipEvent_t> ev;    // pairs (start, stop)
-    std::vector<uint32_t> ev_w;    // rounds covered by each pair (a persistent launch covers several)
+    std::vector<uint32_t> ev_w;    // rounds covered by each pair
     size_t ev_used = 0;
     double timed_ms = 0.0;
     uint64_t timed_launches = 0;
@@ -265,7 +262,6 @@ static void release(acs_sim* s) {
     (void)hipFree(s->xall);
     (void)hipFree(s->ell);
     binned_free(s->bin);
-    persist_free(s->pers);
     generic_big_free(s->big);
     (void)hipFree(s->status);
     (void)hipFree(s->st);
@@ -360,7 +356,7 @@ static int harvest_timing(acs_sim* s) {
     return ACS_OK;
 }
 
-// rounds: how many rounds the bracketed launch covers (the persistent launch covers several)
+// rounds: how many rounds the bracketed launch covers
 static int timing_begin(acs_sim* s, hipEvent_t* e1, uint32_t rounds = 1) {
     *e1 = nullptr;
     if (!s->timing || s->timing_ctr++ % s->timing != 0) return ACS_OK;
@@ -662,7 +658,7 @@ static int flush_finalize(acs_sim* s) {
 }
 
 // roctx range for the rocprofv3 --marker-trace timeline: host-side enqueue spans of
-// round chunks and persistent launches.
+// round chunks and the one-launch batched / dense paths.
 struct RoctxRange {
     explicit RoctxRange(const char* m) { roctxRangePushA(m); }
     ~RoctxRange() { roctxRangePop(); }
@@ -714,53 +710,6 @@ static int advance(acs_sim* s, uint32_t k) {
         HIP_TRY(hipStreamSynchronize(s->stream));
         s->round += k;
         if (s->want_summary) s->h_ndone[0] = s->h_sum->n_done;
-        s->all_done = s->h_ndone[0] == s->B;
-        return ACS_OK;
-    }
-    if (s->pers.on) {   // every requested round in one persistent launch (it stops at the verdict)
-        if (int rc = flush_finalize(s)) return rc;
-        PersistArgs a{};
-        a.idxA = s->bin.idxA;
-        a.invpos = s->bin.invpos;
-        a.tiles = s->bin.tiles;
-        a.aseg = s->pers.aseg;
-        a.stage[0] = s->bin.stage1;
-        a.stage[1] = s->pers.stage2;
-        a.x[0] = xb(s, 0);
-        a.x[1] = xb(s, 1);
-        a.partial[0] = s->partial;
-        a.partial[1] = s->pers.partial2;
-        a.st = s->st;
-        a.trace = s->trace;
-        a.n_done = s->n_done;
-        a.ctl = s->pers.ctl;
-        a.N = s->N;
-        a.tmo = s->pers.tmo;
-        a.SA = s->bin.SA;
-        a.P = s->bin.P;
-        a.Q = s->bin.Q;
-        a.S = s->pers.S;
-        a.NA = s->pers.NA;
-        a.NB = s->pers.NB;
-        a.r0 = s->round;
-        a.k = k;
-        a.max_rounds = s->c.max_rounds;
-        a.term_eps = s->c.termination == ACS_TERM_EPS ? 1u : 0u;
-        a.rule = s->c.rule;
-        a.eps = s->c.eps;
-        hipEvent_t e1;
-        if (int rc = timing_begin(s, &e1, k)) return rc;
-        RoctxRange range("acs: persistent binned rounds");
-        HIP_TRY(launch_round_persist(s->pers, s->bin, a, s->d, s->c.trim, s->stream));
-        if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
-        uint64_t* abort_word = s->pers.ctl + persist_ctl_abort(s->pers, s->bin.P);
-        HIP_TRY(hipMemcpyAsync(s->h_ndone, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
-        HIP_TRY(hipMemcpyAsync(&s->pers_abort, abort_word, sizeof(uint64_t), hipMemcpyDeviceToHost, s->stream));
-        HIP_TRY(hipStreamSynchronize(s->stream));
-        if (s->pers_abort)
-            return fail(ACS_EDEVICE, "persistent binned round: a wait outlived the watchdog (round %u..%u)", s->round,
-                        s->round + k);
-        s->round += k;
         s->all_done = s->h_ndone[0] == s->B;
         return ACS_OK;
     }
@@ -1133,26 +1082,9 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
             s->defer_fin = false;
             s->kname = kname_lane + (s->f32 ? " [f32]" : "");
         }
-        if (s->binned && s->clean && !partitioned && !s->f32 && s->B == 1 && !s->n_hub && !s->csr_var &&
-            cfg->delay_max == 0) {
-            // persistent rounds: opt-in (ACSIM_PERSIST=1) until they beat the
-            // two-kernel round (measured 464 vs 126 µs per cfg4 round, profiles/r03_s1_persist.jsonl)
-            const char* pv = getenv("ACSIM_PERSIST");
-            if (pv && pv[0] == '1') {
-                const hipError_t pe = persist_build(s->pers, s->bin, s->N, s->d, cfg->trim, cfg->rule, s->stream);
-                if (pe != hipSuccess && pe != hipErrorNotSupported) CREATE_TRY(pe);
-                if (s->pers.on) {
-                    s->defer_fin = false;
-                    char nm[96];
-                    snprintf(nm, sizeof nm, "k_bin_persist<%u,%u> S%u NA%u NB%u", s->d, cfg->trim, s->pers.S,
-                             s->pers.NA, s->pers.NB);
-                    s->kname = nm;
-                }
-            }
-        }
         if (s->binned) {
             // NP-pass phase B (slot-dependent configs: fp64, two passes only; see launch_round_binned)
-            if (!s->pers.on && s->bin.split > 1 && (s->clean || (!s->f32 && s->bin.split == 2)))
+            if (s->bin.split > 1 && (s->clean || (!s->f32 && s->bin.split == 2)))
                 s->kname += " split" + std::to_string(s->bin.split);
             if (s->bin.fix) {   // fault fix-up list instead of tagged senders
                 const size_t pos = s->kname.find("+k_bin_tag");

@@ -1,6 +1,5 @@
-// binned_dev.hpp — device pieces shared by the binned exchange (round_binned.hip) and its
-// persistent one-launch form (round_persist.hip): cache-policy switches, the phase-A index stream,
-// the LDS-DMA run copies and the NP-pass image bound.  SURVEY §8(a) a5 / a7.
+// binned_dev.hpp — device pieces of the binned exchange (round_binned.hip): cache-policy switches,
+// the phase-A index stream, the LDS-DMA run copies and the NP-pass image bound.  SURVEY §8(a) a5 / a7.
 #pragma once
 
 #include "finalize.hpp"

@@ -209,59 +209,6 @@ struct SrcSel {
 hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool clean, hipStream_t s,
                                const FinalizeArgs* fin = nullptr, uint32_t phases = 7, SrcSel sel = SrcSel{});
 
-// Persistent binned rounds (round_persist.hip): the clean one-level fp64 exchange
-// of one unpartitioned instance as ONE launch over k rounds.  One 1024-thread workgroup per CU
-// (cooperative launch): NA = P·S "A-workers" each stream one (source block, receiver-block
-// segment) of phase A every round, publishing their progress; the other NB workgroups are
-// "B-workers" whose four 256-thread sub-groups run phase B on receiver blocks as soon as every
-// source block's stream has passed them.  A source block's next round starts as soon as the
-// receiver blocks of its own rows are done, so the phases of consecutive rounds overlap and no
-// kernel boundary, ramp or tail separates them.  The ε fold runs in the last receiver block of a
-// round.  Stage and partials are double-buffered by round parity.
-struct PersistPlan {
-    bool on = false;
-    uint32_t S = 0, NA = 0, NB = 0, NP = 0;   // segments per source block, A- / B-workers, phase-B passes
-    uint64_t* aseg = nullptr;                  // [P*S + 1] stream start of (source block a, segment s)
-    double* stage2 = nullptr;                  // the second stage buffer (odd rounds)
-    double2* partial2 = nullptr;               // the second partial buffer (odd rounds)
-    uint64_t* ctl = nullptr;                   // [nctl] control words, zeroed before every launch
-    uint32_t nctl = 0;
-    uint64_t tmo = 0;                          // watchdog per wait, s_memrealtime ticks (100 MHz)
-    uint64_t* ts = nullptr;                    // ACSIM_PERSIST_TS diagnostic buffer (PersistArgs::ts)
-    uint32_t ts_k = 0;                         // rounds it holds
-};
-struct PersistArgs {
-    const uint16_t* idxA;
-    const uint16_t* invpos;
-    const uint2* tiles;
-    const uint64_t* aseg;
-    double* stage[2];       // stage of round r: stage[r & 1]
-    double* x[2];           // x^r: x[r & 1]
-    double2* partial[2];    // block partials of round r: partial[r & 1]
-    InstState* st;
-    double* trace;          // nullptr if disabled
-    uint32_t* n_done;
-    uint64_t* ctl;          // [NA] progress, [P] receiver blocks done per source block, then
-                            // blocks done, folds done, abort
-    uint64_t N, tmo;
-    uint32_t SA, P, Q, S, NA, NB, r0, k, max_rounds, term_eps, rule;
-    double eps;
-    uint32_t diag;          // diagnostic switches (ACSIM_PERSIST_DIAG, timing only, no publication
-                            // guarantee): bit 0 = A stream stores nontemporal instead of write-through,
-                            // bit 1 = B run copies by default-policy instead of sc1 LDS-DMA
-    uint64_t* ts;           // diagnostic (ACSIM_PERSIST_TS=<file>): [k][NA][3] A-worker (wait start,
-                            // staged, stream end) then [k][Q][3] block (poll start, ready, done), 100 MHz
-};
-// S = 0: choose; returns hipErrorNotSupported when the plan / device does not fit the scheme.
-hipError_t persist_build(PersistPlan& pp, const BinnedPlan& p, uint64_t N, uint32_t d, uint32_t trim, uint32_t rule,
-                         hipStream_t s);
-void persist_free(PersistPlan& pp);
-hipError_t launch_round_persist(const PersistPlan& pp, const BinnedPlan& p, const PersistArgs& a, uint32_t d,
-                                uint32_t trim, hipStream_t s);
-// ctl layout (round_persist.hip): [S * kPersistNch) chunk counters, [P) receiver blocks done per
-// source block, blocks done, folds done, abort
-constexpr uint32_t kPersistNch = 32;
-inline uint64_t persist_ctl_abort(const PersistPlan& pp, uint32_t P) { return (uint64_t)pp.S * kPersistNch + P + 2; }
 
 // Generic kernel: one workgroup per receiver, LDS bitonic sort (any topology, m <= 8192).
 constexpr uint32_t kGenericMaxM = 8192;   // receivers with more entries take the big-m path

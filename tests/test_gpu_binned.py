@@ -145,8 +145,7 @@ def test_faulty_fixup_and_tagged_paths_match_oracle(oracle_mod, name):
 def test_binned_full_cfg4_fixed_matches_per_lane():
     """Full-size headline graph (N = 2^20): 30 FIXED rounds, binned vs per-lane bit for bit."""
     cfg = preset("cfg4", max_rounds=30, trace_spread=True)
-    with env(ACSIM_PERSIST=0):   # the two-kernel round (the persistent one: tests/test_gpu_persist.py)
-        kb, rb, xb, tb = run_gpu(cfg)
+    kb, rb, xb, tb = run_gpu(cfg)
     assert kb.startswith("k_bin_scatter"), kb
     with env(ACSIM_BINNED=0):
         _, rr, xr, tr = run_gpu(cfg)
