@@ -698,18 +698,15 @@ static int advance(acs_sim* s, uint32_t k) {
         else
             HIP_TRY(launch_batched_small(a, s->B, k, s->stream));
         if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
-        if (s->want_summary) {
-            // acs_run: the result summary and the done count ride on the same synchronisation, in
-            // one launch that writes host memory (no copies: each costs a DMA round trip, which
-            // bounded the per-rank time of small cfg3 shards)
-            HIP_TRY(launch_run_summary_mapped(s->st, s->B, s->n_done, s->sum_scratch, s->h_sum_dev, s->stream));
-            s->summary_ready = true;
-        } else {
-            HIP_TRY(hipMemcpyAsync(s->h_ndone, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
-        }
+        // The done count (and, for acs_run, the result summary) ride on the same synchronisation,
+        // folded from the instances' done flags in one launch that writes host memory: no copies
+        // (each costs a DMA round trip) and no per-instance atomic on one counter (the batched
+        // kernels' last generation finished together and serialised on it), DESIGN.md §6
+        HIP_TRY(launch_run_summary_mapped(s->st, s->B, s->sum_scratch, s->h_sum_dev, s->stream));
+        s->summary_ready = s->want_summary;
         HIP_TRY(hipStreamSynchronize(s->stream));
         s->round += k;
-        if (s->want_summary) s->h_ndone[0] = s->h_sum->n_done;
+        s->h_ndone[0] = s->h_sum->n_done;
         s->all_done = s->h_ndone[0] == s->B;
         return ACS_OK;
     }
@@ -1326,7 +1323,7 @@ int acs_run(acs_sim* s, acs_result* out) {
     const auto t1 = std::chrono::steady_clock::now();
     if (out) {   // the summary is folded on the device: 32 bytes back instead of B states
         if (!s->summary_ready) {
-            HIP_TRY(launch_run_summary_mapped(s->st, s->B, nullptr, s->sum_scratch, s->h_sum_dev, s->stream));
+            HIP_TRY(launch_run_summary_mapped(s->st, s->B, s->sum_scratch, s->h_sum_dev, s->stream));
             HIP_TRY(hipStreamSynchronize(s->stream));
         }
         s->summary_ready = false;

@@ -135,14 +135,12 @@ __global__ __launch_bounds__(64) void k_batched_mfma(const BatchArgs a, uint32_t
         if (node < N) xout[node] = xb[s];
     }
     if (h == 0) {
-        const bool was_done = S->done != 0;
         S->lo = lo;
         S->hi = hi;
         S->spread = spread;
         S->rounds = r;
         S->converged = conv ? 1u : 0u;
         S->done = done ? 1u : 0u;
-        if (done && !was_done) atomicAdd(a.n_done, 1u);
     }
 }
 

@@ -280,7 +280,6 @@ __global__ __launch_bounds__(64, (!SORT && !FAULTS) ? ACS_BATCHED_WPE : 1) void 
         S->rounds = r;
         S->converged = conv ? 1u : 0u;
         S->done = done ? 1u : 0u;
-        if (done) atomicAdd(a.n_done, 1u);
     }
 }
 
@@ -406,7 +405,6 @@ __global__ __launch_bounds__(64 * F, (F == 2 && sizeof(VT) == 8 && ACS_SPLIT_WPE
         S->rounds = r;
         S->converged = conv ? 1u : 0u;
         S->done = done ? 1u : 0u;
-        if (done) atomicAdd(a.n_done, 1u);
     }
 }
 

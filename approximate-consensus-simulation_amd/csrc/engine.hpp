@@ -128,15 +128,15 @@ hipError_t launch_partials_from_x(const double* x, const uint32_t* status, uint6
                                   double2* partial, uint32_t nblk, bool f32, hipStream_t s);
 hipError_t launch_finalize(const FinalizeArgs& a, uint64_t B, hipStream_t s);
 struct RunSummary {   // acs_run's result, folded on the device (32 bytes)
-    unsigned int rounds_max, n_done;   // (n_done: written by the one-launch form only)
+    unsigned int rounds_max, n_done;   // n_done: instances whose done flag is set
     unsigned long long n_converged, rounds_sum, spread_max_bits;
 };
 // acs_run's summary in ONE launch with no copy: block partials, then the last block to arrive folds
-// them and stores the summary (and *n_done) straight into host-mapped memory `out`.  scratch: a
-// device buffer of kSummaryScratch bytes whose first word is zero (the last block re-zeroes it).
-constexpr uint32_t kSummaryScratch = 1024 * 32 + 64;
-hipError_t launch_run_summary_mapped(const InstState* st, uint64_t B, const uint32_t* n_done, void* scratch,
-                                     RunSummary* out, hipStream_t s);
+// them and stores the summary (with the count of done instances) straight into host-mapped memory
+// `out`.  scratch: a device buffer of kSummaryScratch bytes whose first word is zero (the last block
+// re-zeroes it).
+constexpr uint32_t kSummaryScratch = 1024 * 48 + 64;
+hipError_t launch_run_summary_mapped(const InstState* st, uint64_t B, void* scratch, RunSummary* out, hipStream_t s);
 
 // ---- round kernels
 // Register-resident kernel for RANDOM_REGULAR with a compiled (d, t) pair; returns

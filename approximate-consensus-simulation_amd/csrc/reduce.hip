@@ -45,20 +45,21 @@ __global__ __launch_bounds__(kReduceBlock) void k_finalize(const FinalizeArgs a)
 struct SumPart {
     uint32_t rmax, conv;
     uint64_t rsum, smax;
+    uint32_t ndone, pad;
 };
 __global__ __launch_bounds__(kReduceBlock) void k_run_summary_mapped(const InstState* __restrict__ st, uint64_t B,
-                                                                     const uint32_t* __restrict__ n_done,
                                                                      unsigned char* scratch, RunSummary* out) {
     uint32_t* cnt = reinterpret_cast<uint32_t*>(scratch);
     SumPart* part = reinterpret_cast<SumPart*>(scratch + 64);
     __shared__ SumPart red[kReduceBlock / 64];
     __shared__ uint32_t last;
-    uint32_t rmax = 0, conv = 0;
+    uint32_t rmax = 0, conv = 0, dn = 0;
     uint64_t rsum = 0, smax = 0;
     for (uint64_t b = (uint64_t)blockIdx.x * kReduceBlock + threadIdx.x; b < B; b += (uint64_t)gridDim.x * kReduceBlock) {
         const InstState e = st[b];
         rmax = e.rounds > rmax ? e.rounds : rmax;
         conv += e.converged;
+        dn += e.done != 0u;
         rsum += e.rounds;
         const uint64_t sb = (uint64_t)__double_as_longlong(e.spread);
         smax = sb > smax ? sb : smax;
@@ -71,24 +72,26 @@ __global__ __launch_bounds__(kReduceBlock) void k_run_summary_mapped(const InstS
             rmax = r2 > rmax ? r2 : rmax;
             smax = s2 > smax ? s2 : smax;
             conv += __shfl_xor(conv, o, 64);
+            dn += __shfl_xor(dn, o, 64);
             rsum += __shfl_xor(rsum, o, 64);
         }
     };
     auto fold_block = [&]() {   // -> thread 0
         fold_wave();
-        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = SumPart{rmax, conv, rsum, smax};
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = SumPart{rmax, conv, rsum, smax, dn, 0u};
         __syncthreads();
         if (threadIdx.x == 0)
             for (uint32_t w = 1; w < kReduceBlock / 64; ++w) {
                 rmax = red[w].rmax > rmax ? red[w].rmax : rmax;
                 smax = red[w].smax > smax ? red[w].smax : smax;
                 conv += red[w].conv;
+                dn += red[w].ndone;
                 rsum += red[w].rsum;
             }
     };
     fold_block();
     if (threadIdx.x == 0) {
-        part[blockIdx.x] = SumPart{rmax, conv, rsum, smax};
+        part[blockIdx.x] = SumPart{rmax, conv, rsum, smax, dn, 0u};
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == gridDim.x;
@@ -98,19 +101,20 @@ __global__ __launch_bounds__(kReduceBlock) void k_run_summary_mapped(const InstS
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    rmax = 0, conv = 0, rsum = 0, smax = 0;
+    rmax = 0, conv = 0, dn = 0, rsum = 0, smax = 0;
     for (uint32_t k = threadIdx.x; k < gridDim.x; k += kReduceBlock) {
         const SumPart q = part[k];
         rmax = q.rmax > rmax ? q.rmax : rmax;
         smax = q.smax > smax ? q.smax : smax;
         conv += q.conv;
+        dn += q.ndone;
         rsum += q.rsum;
     }
     __syncthreads();   // (red[] reuse)
     fold_block();
     if (threadIdx.x == 0) {
         out->rounds_max = rmax;
-        out->n_done = n_done ? *n_done : 0u;
+        out->n_done = dn;
         out->n_converged = conv;
         out->rounds_sum = rsum;
         out->spread_max_bits = smax;
@@ -118,12 +122,11 @@ __global__ __launch_bounds__(kReduceBlock) void k_run_summary_mapped(const InstS
     }
 }
 
-hipError_t launch_run_summary_mapped(const InstState* st, uint64_t B, const uint32_t* n_done, void* scratch,
-                                     RunSummary* out, hipStream_t s) {
+hipError_t launch_run_summary_mapped(const InstState* st, uint64_t B, void* scratch, RunSummary* out, hipStream_t s) {
     const uint64_t g = (B + kReduceBlock - 1) / kReduceBlock;
     static_assert(64 + 1024 * sizeof(SumPart) <= kSummaryScratch, "summary scratch");
     hipLaunchKernelGGL(k_run_summary_mapped, dim3((unsigned)(g == 0 ? 1 : g < 1024 ? g : 1024)), dim3(kReduceBlock), 0, s,
-                       st, B, n_done, reinterpret_cast<unsigned char*>(scratch), out);
+                       st, B, reinterpret_cast<unsigned char*>(scratch), out);
     return hipGetLastError();
 }
 
