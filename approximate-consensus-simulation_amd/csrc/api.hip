@@ -92,6 +92,7 @@ struct acs_sim {
     RunSummary* h_sum = nullptr;   // pinned, host-mapped: the one-launch summary writes it directly
     RunSummary* h_sum_dev = nullptr;   // h_sum's device address
     void* sum_scratch = nullptr;       // launch_run_summary_mapped's partials and arrival counter
+    unsigned long long* eacc = nullptr;   // [2][kEaccWords] published EPS verdicts (RoundArgs::eacc), by round parity
     bool want_summary = false;     // acs_run on a one-launch path: enqueue the summary before the sync
     bool summary_ready = false;    // h_sum holds the summary of the current state
     uint32_t round = 0;            // round of every unfinished instance
@@ -281,6 +282,7 @@ static void release(acs_sim* s) {
     if (s->h_ndone) (void)hipHostFree(s->h_ndone);
     (void)hipFree(s->sum_scratch);
     if (s->h_sum) (void)hipHostFree(s->h_sum);
+    if (s->eacc) (void)hipFree(s->eacc);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
 }
@@ -525,9 +527,17 @@ static int enqueue_round(acs_sim* s, uint32_t r) {
     hipEvent_t e1;
     int rc = timing_begin(s, &e1);
     if (rc) return rc;
+    // EPS verdict publication: phase B of round r folds its exact (min, max) into
+    // eacc[(r + 1) & 1], so every workgroup of round r + 1's phase A can stop on convergence
+    // (without it only workgroup 0 folds the partials and the others stream one last round)
+    unsigned long long* pub = s->eacc && s->binned && s->defer_fin && !s->n_hub && !s->partitioned &&
+                                      s->c.termination == ACS_TERM_EPS
+                                  ? s->eacc + kEaccWords * ((r + 1) & 1u)
+                                  : nullptr;
     if (!s->partitioned) {
         if (s->binned) {
             RoundArgs ab = a;
+            ab.eacc = pub;
             if (s->n_hub) ab.qhi = s->nblk_fast;   // the hub rows' partial slots are the generic kernel's
             HIP_TRY(launch_round_binned(s->bin, ab, s->clean, s->stream, s->fin_pending ? &s->fin_args : nullptr));
             s->fin_pending = false;
@@ -572,6 +582,7 @@ static int enqueue_round(acs_sim* s, uint32_t r) {
         const FinalizeArgs fin = make_finalize(s, r + 1, s->partial, s->nblk, false);
         if (s->defer_fin) {   // folded by the next round's phase A, or by flush_finalize
             s->fin_args = fin;
+            s->fin_args.eacc = pub;
             s->fin_pending = true;
             return ACS_OK;
         }
@@ -1006,6 +1017,13 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     CREATE_TRY(hipHostMalloc(&s->h_sum, sizeof(RunSummary), hipHostMallocMapped | hipHostMallocPortable));
     CREATE_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&s->h_sum_dev), s->h_sum, 0));
     CREATE_TRY(hipMalloc(&s->sum_scratch, kSummaryScratch));
+    {
+        const char* v = getenv("ACSIM_EPS_PUB");
+        if (!(v && v[0] == '0')) {
+            CREATE_TRY(hipMalloc(&s->eacc, 2 * kEaccWords * sizeof(unsigned long long)));
+            CREATE_TRY(hipMemsetAsync(s->eacc, 0, 2 * kEaccWords * sizeof(unsigned long long), s->stream));
+        }
+    }
     CREATE_TRY(hipMemsetAsync(s->sum_scratch, 0, kSummaryScratch, s->stream));
     if (cfg->trace_spread) {
         const uint64_t nt = s->B * ((uint64_t)cfg->max_rounds + 1);

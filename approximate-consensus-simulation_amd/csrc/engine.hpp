@@ -71,7 +71,13 @@ struct RoundArgs {
     const uint32_t* crank;
     const uint32_t* clist;
     uint32_t coff;
+    // EPS verdict publication (binned phase B): non-null: every block also folds its
+    // (min, max) into eacc[0] = max ~ord(min), eacc[1] = max ord(max) (ord: order-preserving bits,
+    // identity 0), so the next phase A's workgroups can stop without the block partials
+    unsigned long long* eacc;
 };
+constexpr uint32_t kEaccSlots = 32, kEaccStride = 16;       // eacc pairs, u64 words between pairs
+constexpr uint32_t kEaccWords = kEaccSlots * kEaccStride;   // eacc words of one round parity
 
 constexpr uint32_t kEllNone = 0xFFFFFFFFu;   // padding column of a CSR row below the compiled degree
 constexpr uint8_t kDegHub = 0xFF;             // deg[] of a CSR hub row (above the compiled degree): the fast
@@ -92,6 +98,7 @@ struct FinalizeArgs {
     uint32_t init_mode;       // 1: (re)initialisation, ignores the done flag
     uint32_t negmin;          // 1: partial[k].x holds -min (after an all-reduce MAX of (-min, max))
     double2* fold_out;        // non-null: only fold the partials into (-min, max) here (node partition)
+    const unsigned long long* eacc;   // binned phase A: the verdict the previous phase B published (or null)
 };
 
 struct BatchArgs {

@@ -57,16 +57,38 @@ __device__ __forceinline__ double wave_max(double v) {
     return v;
 }
 
+// EPS verdict publication (RoundArgs::eacc): a double's bits mapped so that unsigned order is numeric
+// order (for non-NaN values), and back.  Block b folds into pair b % kEaccSlots (one 128-B line each,
+// so the blocks' device-scope atomics spread over 32 addresses instead of queueing on one); word 0
+// holds max ~ord(min), word 1 max ord(max), both with identity 0.  A reader takes the max over the
+// pairs; if nothing was published the pair decodes to NaNs, whose spread never passes the ε test.
+__device__ __forceinline__ unsigned long long ord_of(double v) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    return (u >> 63) ? ~u : (u | (1ull << 63));
+}
+__device__ __forceinline__ double ord_inv(unsigned long long o) {
+    return __longlong_as_double((long long)((o >> 63) ? (o & ~(1ull << 63)) : ~o));
+}
+__device__ __forceinline__ void publish_minmax(unsigned long long* eacc, double mn, double mx) {
+    unsigned long long* p = eacc + (blockIdx.x % kEaccSlots) * kEaccStride;
+    __hip_atomic_fetch_max(p, ~ord_of(mn), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_max(p + 1, ord_of(mx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Block-wide honest (min, max) -> one partial per block (§A.8; min/max are exact and
-// order-free, so any reduction tree gives the oracle's value).
+// order-free, so any reduction tree gives the oracle's value).  eacc: also publish it (above).
 template <int BS>
-__device__ __forceinline__ void block_minmax_store(double mn, double mx, double2* out) {
+__device__ __forceinline__ void block_minmax_store(double mn, double mx, double2* out,
+                                                   unsigned long long* eacc = nullptr) {
     static_assert(BS % 64 == 0, "block must be whole wavefronts");
     constexpr int NW = BS / 64;
     mn = wave_min(mn);
     mx = wave_max(mx);
     if constexpr (NW == 1) {
-        if (threadIdx.x == 0) *out = make_double2(mn, mx);
+        if (threadIdx.x == 0) {
+            *out = make_double2(mn, mx);
+            if (eacc) publish_minmax(eacc, mn, mx);
+        }
     } else {
         __shared__ double2 red[NW];
         const int w = threadIdx.x >> 6;
@@ -80,6 +102,7 @@ __device__ __forceinline__ void block_minmax_store(double mn, double mx, double2
                 c = __builtin_fmax(c, red[k].y);
             }
             *out = make_double2(a, c);
+            if (eacc) publish_minmax(eacc, a, c);
         }
     }
 }

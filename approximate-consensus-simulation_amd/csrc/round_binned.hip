@@ -47,10 +47,17 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
                                                      const InstState* __restrict__ st, uint64_t N, uint32_t SA,
                                                      uint32_t segs, uint32_t chunk, uint32_t pol,
                                                      const FinalizeArgs fin, uint32_t fin_on, const SrcSel sel,
-                                                     uint64_t* __restrict__ ts) {
+                                                     uint64_t* __restrict__ ts, unsigned long long* __restrict__ ereset) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lx_raw[];
     VT* lx = reinterpret_cast<VT*>(lx_raw);
     if (st->done) return;
+    // this round's phase B publishes its verdict into ereset (the pair the previous phase B filled is
+    // fin.eacc, read below; the next phase A reads this one)
+    if (ereset && blockIdx.x == 0 && threadIdx.x < kEaccSlots) {
+        unsigned long long* e = ereset + threadIdx.x * kEaccStride;
+        __hip_atomic_store(e, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(e + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     const uint64_t t0 = ts ? __builtin_amdgcn_s_memrealtime() : 0;
     // XCD-aware order (dispatch deals blocks round-robin over the 8 XCDs): every segment of source
     // block a runs on the XCD of blockIdx % 8 = a % 8, so its x block is fetched into one L2 once
@@ -80,16 +87,39 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
     if (fin_on) {
         // deferred finalize of the previous round.  Only workgroup 0 folds the
         // partials and records the verdict (the loads overlap the x staging above; the fold's
-        // barrier drains both).  The other workgroups stream unconditionally unless the round
-        // cap is reached: if the EPS test has just ended the run, their stage is never read,
-        // because phase B (the next launch) sees the done flag workgroup 0 set and exits, and
-        // every later launch exits at its first line.  A finished instance stops here.
+        // barrier drains both).  The other workgroups take the verdict the previous phase B
+        // published (fin.eacc: the same exact min / max, so the same ε test), or without one stream
+        // unconditionally unless the round cap is reached: if the EPS test has just ended the run,
+        // their stage is never read, because phase B (the next launch) sees the done flag
+        // workgroup 0 set and exits, and every later launch exits at its first line.  A finished
+        // instance stops here.
         bool done;
         if (blockIdx.x == 0) {
             done = fold_partials<false, kBinA>(fin, 0, true);
         } else {
+            // (plain loads: the previous phase B's atomics completed before this launch began, and
+            // the kernel boundary makes them visible here as it does x^r itself)
+            __shared__ uint32_t pub_done;
+            if (threadIdx.x < 64) {
+                unsigned long long lo = 0, hi = 0;
+                if (fin.eacc && threadIdx.x < kEaccSlots) {
+                    lo = fin.eacc[threadIdx.x * kEaccStride];
+                    hi = fin.eacc[threadIdx.x * kEaccStride + 1];
+                }
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) {
+                    const unsigned long long l2 = __shfl_xor(lo, o, 64), h2 = __shfl_xor(hi, o, 64);
+                    lo = l2 > lo ? l2 : lo;
+                    hi = h2 > hi ? h2 : hi;
+                }
+                if (threadIdx.x == 0) {
+                    const double mn = ord_inv(~lo), mx = ord_inv(hi);
+                    const double spread = fin.f32 ? (double)(float)(mx - mn) : mx - mn;
+                    pub_done = fin.eacc && fin.term_eps && spread <= fin.eps ? 1u : 0u;
+                }
+            }
             __syncthreads();
-            done = fin.r_next >= fin.max_rounds;
+            done = pub_done != 0u || fin.r_next >= fin.max_rounds;
         }
         if (done || idle) return;
     } else {
@@ -452,7 +482,7 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
             mx = res;
         }
     }
-    block_minmax_store<kBinSB>(mn, mx, a.partial + b);
+    block_minmax_store<kBinSB>(mn, mx, a.partial + b, a.eacc);
     if (a.ts) bin_ts(a.ts, t0, t1);
 }
 
@@ -611,7 +641,7 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather_of(const RoundArgs a, con
         mn = res;
         mx = res;
     }
-    block_minmax_store<kBinSB>(mn, mx, a.partial + b);
+    block_minmax_store<kBinSB>(mn, mx, a.partial + b, a.eacc);
 }
 
 // ------------------------------------------------------------------------------ plan build
@@ -1249,7 +1279,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
         }
         if (phases & 1)
             hipLaunchKernelGGL(k_bin_scatter<float>, dim3((nsrc + 7) / 8 * 8 * p.segs), dim3(kBinA), p.SA * sizeof(float), s,
-                               fsrc, p.idxA, p.aoff, st1, a.st, a.N, p.SA, p.segs, p.chunk, pol, fa, fin_on, sel, p.ts);
+                               fsrc, p.idxA, p.aoff, st1, a.st, a.N, p.SA, p.segs, p.chunk, pol, fa, fin_on, sel, p.ts, a.eacc);
         if (p.levels == 2) {
             float* st2 = reinterpret_cast<float*>(p.stage2);
             if (phases & 2)
@@ -1308,7 +1338,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
     }
     if (phases & 1)
         hipLaunchKernelGGL(k_bin_scatter<double>, dim3((nsrc + 7) / 8 * 8 * p.segs), dim3(kBinA), p.SA * sizeof(double), s, src,
-                           p.idxA, p.aoff, p.stage1, a.st, a.N, p.SA, p.segs, p.chunk, pol, fa, fin_on, sel, p.ts);
+                           p.idxA, p.aoff, p.stage1, a.st, a.N, p.SA, p.segs, p.chunk, pol, fa, fin_on, sel, p.ts, a.eacc);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const double* last = p.stage1;

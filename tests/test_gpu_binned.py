@@ -293,24 +293,25 @@ def test_cache_policy_switches_bit_exact(oracle_mod, pol):
 @pytest.mark.parametrize("term", ["eps", "fixed"])
 def test_deferred_finalize_matches_standalone(oracle_mod, term):
     """The default folds a round's spread inside the next round's phase A (ACSIM_DEFER_FIN=0:
-    a k_finalize launch per round).  Rounds, traces and values must agree with each other and the
-    oracle, across round(k) calls that end mid-chunk."""
+    a k_finalize launch per round), and under EPS phase B publishes its verdict for the other
+    phase-A workgroups (ACSIM_EPS_PUB=0: they stream one last round).  Rounds, traces and values
+    must agree with each other and the oracle, across round(k) calls that end mid-chunk."""
     cfg = Config(n_nodes=40000, topology="regular", degree=32, rule="trimmed", trim=5, eps=1e-9,
                  termination=term, max_rounds=37, seed=12, trace_spread=True)
     out = {}
-    for d in (1, 0):
-        with env(ACSIM_BIN_SA=2048, ACSIM_DEFER_FIN=d):
+    for d, pub in ((1, 1), (1, 0), (0, 1)):
+        with env(ACSIM_BIN_SA=2048, ACSIM_DEFER_FIN=d, ACSIM_EPS_PUB=pub):
             with acsim.Simulator(cfg, device=0) as g:
                 g.round(5)
                 g.round(19)
                 g.run()
-                out[d] = (g.rounds(), bits(g.values(0)), bits(g.spread_trace(0)))
+                out[d, pub] = (g.rounds(), bits(g.values(0)), bits(g.spread_trace(0)))
     with oracle_mod.OracleSimulator(cfg, threads=8) as o:
         o.run()
         ref = (o.rounds(), bits(o.values(0)), bits(o.spread_trace(0)))
-    for d in (1, 0):
-        for got, want in zip(out[d], ref):
-            assert np.array_equal(got, want), d
+    for key, got3 in out.items():
+        for got, want in zip(got3, ref):
+            assert np.array_equal(got, want), key
 
 
 SPLIT_CASES = ["d32_t5_eps_n50000_sa1024", "d16_t5_fixed_odd_sa512", "d8_t2_midpoint_sa256",
