@@ -17,6 +17,11 @@ length-prefixed msgpack (bytes, ints, floats, strings, lists, dicts; tuples arri
 Rendezvous: `Group.from_env()` reads RANK / WORLD_SIZE / MASTER_ADDR as torch.distributed.run sets
 them and listens on MASTER_PORT + 1 (torch's launcher keeps its own store on MASTER_PORT), or on
 ACSIM_RDZV_PORT when that is set.
+
+Hardening (the listener is unauthenticated): a message may not exceed ACSIM_RDZV_MAX_MSG bytes
+(64 MiB by default), so a stray connection cannot make rank 0 allocate arbitrary memory; the
+listener binds to the loopback interface when MASTER_ADDR is local (127.0.0.0/8 or localhost);
+and when ACSIM_RDZV_TOKEN is set, every rank's hello must carry the same token.
 """
 from __future__ import annotations
 
@@ -30,6 +35,7 @@ import msgpack
 import numpy as np
 
 _HDR = struct.Struct("<Q")
+_MAX_MSG = int(os.environ.get("ACSIM_RDZV_MAX_MSG", str(64 << 20)))
 
 
 def _send(sock: socket.socket, obj: Any) -> None:
@@ -49,14 +55,21 @@ def _recv_exact(sock: socket.socket, n: int) -> bytes:
 
 def _recv(sock: socket.socket) -> Any:
     (n,) = _HDR.unpack(_recv_exact(sock, _HDR.size))
+    if n > _MAX_MSG:
+        raise ConnectionError(f"rendezvous: message of {n} B exceeds the {_MAX_MSG} B cap "
+                              f"(ACSIM_RDZV_MAX_MSG)")
     return msgpack.unpackb(_recv_exact(sock, n), raw=False)
+
+
+def _is_local(addr: str) -> bool:
+    return addr == "localhost" or addr.startswith("127.")
 
 
 class Group:
     """A fixed set of `world` ranks exchanging small messages through rank 0."""
 
     def __init__(self, rank: int, world: int, addr: str = "127.0.0.1", port: int = 29501,
-                 timeout: float = 600.0):
+                 timeout: float = 600.0, token: Optional[str] = None):
         if world < 1 or not (0 <= rank < world):
             raise ValueError(f"bad rank {rank} / world {world}")
         self.rank, self.world = rank, world
@@ -69,7 +82,13 @@ class Group:
         if rank == 0:
             srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
             srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
-            srv.bind((addr, port))
+            try:
+                srv.bind(("127.0.0.1" if _is_local(addr) else addr, port))
+            except OSError as e:
+                srv.close()
+                raise ConnectionError(
+                    f"rendezvous: rank 0 cannot listen on {addr}:{port} ({e}); the port defaults to "
+                    f"MASTER_PORT + 1 — set ACSIM_RDZV_PORT to a free port") from e
             srv.listen(world)
             srv.settimeout(max(1.0, deadline - time.monotonic()))
             self._srv = srv
@@ -78,10 +97,12 @@ class Group:
                 c, _a = srv.accept()
                 c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
                 c.settimeout(timeout)
-                r = _recv(c)
-                if not isinstance(r, int) or not (1 <= r < world) or peers[r - 1] is not None:
+                hello = _recv(c)
+                r = hello[0] if isinstance(hello, list) and len(hello) == 2 else None
+                if (not isinstance(r, int) or not (1 <= r < world) or peers[r - 1] is not None
+                        or hello[1] != token):
                     c.close()
-                    raise ConnectionError(f"rendezvous: unexpected hello {r!r}")
+                    raise ConnectionError(f"rendezvous: unexpected hello {hello!r}")
                 peers[r - 1] = c
             self._peers = peers  # type: ignore[assignment]
         else:
@@ -97,7 +118,7 @@ class Group:
                     time.sleep(0.05)
             c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
             c.settimeout(timeout)
-            _send(c, rank)
+            _send(c, [rank, token])
             self._up = c
 
     @classmethod
@@ -109,7 +130,7 @@ class Group:
             port = int(os.environ["ACSIM_RDZV_PORT"])
         else:
             port = int(os.environ.get("MASTER_PORT", "29500")) + 1
-        return cls(rank, world, addr, port, timeout)
+        return cls(rank, world, addr, port, timeout, os.environ.get("ACSIM_RDZV_TOKEN"))
 
     # ---- collectives (every rank calls them in the same order)
     def all_gather(self, obj: Any) -> list:

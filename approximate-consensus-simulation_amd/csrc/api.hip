@@ -143,7 +143,6 @@ struct acs_sim {
     uint32_t timing = 0;           // 0 off, else bracket every timing-th round (sampling)
     uint64_t timing_ctr = 0;
     std::vector<hipEvent_t> ev;    // pairs (start, stop)
-    std::vector<uint32_t> ev_w;    // rounds covered by each pair
     size_t ev_used = 0;
     double timed_ms = 0.0;
     uint64_t timed_launches = 0;
@@ -352,22 +351,21 @@ static int harvest_timing(acs_sim* s) {
         float ms = 0.f;
         HIP_TRY(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
         s->timed_ms += ms;
-        s->timed_launches += k / 2 < s->ev_w.size() ? s->ev_w[k / 2] : 1u;
+        s->timed_launches += 1;
     }
     s->ev_used = 0;
     return ACS_OK;
 }
 
-// rounds: how many rounds the bracketed launch covers
-static int timing_begin(acs_sim* s, hipEvent_t* e1, uint32_t rounds = 1) {
+// one bracketed launch (the binned pair of a round, one partition round, or one batched / dense
+// launch covering a whole round(k) call: acs_get_kernel_timing counts launches, not rounds)
+static int timing_begin(acs_sim* s, hipEvent_t* e1) {
     *e1 = nullptr;
     if (!s->timing || s->timing_ctr++ % s->timing != 0) return ACS_OK;
     if (s->ev_used + 2 > 4096) {
         int rc = harvest_timing(s);
         if (rc) return rc;
     }
-    if (s->ev_w.size() < s->ev_used / 2 + 1) s->ev_w.resize(s->ev_used / 2 + 1);
-    s->ev_w[s->ev_used / 2] = rounds;
     hipEvent_t e0 = next_event(s);
     *e1 = next_event(s);
     if (!e0 || !*e1) return fail(ACS_EDEVICE, "hipEventCreate failed");
@@ -529,7 +527,13 @@ static int enqueue_round(acs_sim* s, uint32_t r) {
     if (rc) return rc;
     // EPS verdict publication: phase B of round r folds its exact (min, max) into
     // eacc[(r + 1) & 1], so every workgroup of round r + 1's phase A can stop on convergence
-    // (without it only workgroup 0 folds the partials and the others stream one last round)
+    // (without it only workgroup 0 folds the partials and the others stream one last round).
+    // Invariant: EVERY kernel that writes a.partial in such a round must also publish into ab.eacc
+    // (block_minmax_store(..., a.eacc)): k_bin_gather in all its forms (NP = 1 / 2, VAR, FIX,
+    // FAULTY) and k_bin_gather_of.  A writer that skipped it would not crash: phase A's other
+    // workgroups would stop on a stale verdict while workgroup 0 streams.  Hub rows (generic
+    // kernel partials) and partitioned rounds are therefore excluded here;
+    // tests/test_gpu_binned.py::test_eps_publication_in_every_gather_variant covers each form.
     unsigned long long* pub = s->eacc && s->binned && s->defer_fin && !s->n_hub && !s->partitioned &&
                                       s->c.termination == ACS_TERM_EPS
                                   ? s->eacc + kEaccWords * ((r + 1) & 1u)

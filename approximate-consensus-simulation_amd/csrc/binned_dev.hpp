@@ -63,12 +63,15 @@ __device__ __forceinline__ void bin_store(V2* dst, const V2& v, bool nt) {
 }
 
 // VT = double, or float for fp32 plans (the instruction's store is then 8 bytes)
-// smode: 0 plain stores, 1 nontemporal, 2 write-through (sc1)
-template <typename VT = double>
-__device__ __forceinline__ void bin_stream(const VT* lx, const uint16_t* __restrict__ idx, VT* __restrict__ out,
-                                           uint64_t p0, uint64_t p1, uint32_t smode = 0) {
+// SMODE: 0 plain stores, 1 nontemporal, 2 write-through (sc1) — a template parameter, so the stream
+// loop carries no per-store branch and no buffer descriptor unless it writes through (round 3 had
+// it as a runtime argument: cfg5's phase M and round measured 2-5 % slower)
+template <uint32_t SMODE, typename VT = double>
+__device__ __forceinline__ void bin_stream_t(const VT* lx, const uint16_t* __restrict__ idx, VT* __restrict__ out,
+                                             uint64_t p0, uint64_t p1) {
     using V2 = decltype(bin_pair(VT(0), VT(0)));
-    const bool nt_store = smode == 1;
+    constexpr bool nt_store = SMODE == 1;
+    constexpr uint32_t smode = SMODE;
     constexpr uint32_t SUP = kBinA / 64 * 512, SUPW = SUP / 2;
     constexpr uint32_t SB = 1;   // super-steps per pipelined batch
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -89,9 +92,10 @@ __device__ __forceinline__ void bin_stream(const VT* lx, const uint16_t* __restr
         // super-step's stores in flight across the loop head — first indices consumed before the
         // loop — 67 us; the loop kept rolled 62 us)
         // write-through stores go through a descriptor based at this range (offsets < 4 GiB)
+        // (unused, and dropped by the compiler, unless SMODE == 2)
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            out + p0, 0, (int)((p1 - p0) * sizeof(VT) < 0x7FFFFFF0ull ? (p1 - p0) * sizeof(VT) : 0x7FFFFFF0ull),
-            0x00020000);
+                out + p0, 0, (int)((p1 - p0) * sizeof(VT) < 0x7FFFFFF0ull ? (p1 - p0) * sizeof(VT) : 0x7FFFFFF0ull),
+                0x00020000);
         const uint32_t ob = (w * 256 + lane) * (uint32_t)sizeof(V2);   // this lane's byte offset in a super-step
         for (uint64_t bi = 0; bi < nb; ++bi) {
             // next batch's indices (the last batch re-reads itself: no branch around the loads)
@@ -106,7 +110,7 @@ __device__ __forceinline__ void bin_stream(const VT* lx, const uint16_t* __restr
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const V2 v = bin_pair(lx[c[u][q] & 0xFFFFu], lx[c[u][q] >> 16]);
-                    if (smode == 2)
+                    if constexpr (smode == 2)
                         bin_store_sc1(rs, ob + (uint32_t)(((bi * SB + u) * SUPW + q * 64) * sizeof(V2)), v);
                     else
                         bin_store(op + (bi * SB + u) * SUPW + q * 64, v, nt_store);
@@ -127,6 +131,18 @@ __device__ __forceinline__ void bin_stream(const VT* lx, const uint16_t* __restr
         p = p0 + nsup * SUP;
     }
     for (uint64_t q = p + threadIdx.x; q < p1; q += blockDim.x) out[q] = lx[idx[q]];
+}
+
+// runtime store policy -> the matching instantiation (the branch is taken once per workgroup)
+template <typename VT = double>
+__device__ __forceinline__ void bin_stream(const VT* lx, const uint16_t* __restrict__ idx, VT* __restrict__ out,
+                                           uint64_t p0, uint64_t p1, uint32_t smode = 0) {
+    if (smode == 1)
+        bin_stream_t<1>(lx, idx, out, p0, p1);
+    else if (smode == 2)
+        bin_stream_t<2>(lx, idx, out, p0, p1);
+    else
+        bin_stream_t<0>(lx, idx, out, p0, p1);
 }
 
 // Copy runs [r0, r1) of a run table (start in `src` elements, element offset `pre` in the LDS

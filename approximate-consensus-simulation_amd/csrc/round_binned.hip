@@ -92,7 +92,8 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
         // unconditionally unless the round cap is reached: if the EPS test has just ended the run,
         // their stage is never read, because phase B (the next launch) sees the done flag
         // workgroup 0 set and exits, and every later launch exits at its first line.  A finished
-        // instance stops here.
+        // instance stops here.  (Every writer of the partials publishes: see the invariant where
+        // api.hip enqueue_round chooses `pub`.)
         bool done;
         if (blockIdx.x == 0) {
             done = fold_partials<false, kBinA>(fin, 0, true);

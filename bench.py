@@ -60,6 +60,9 @@ BYTES_PER_NODE_ROUND = 400  # 32*4 + 32*8 + 8 + 8
 BYTES_PER_NODE_ROUND_F32 = 264  # SURVEY §8(d) fp32 mode: 32*4 + 32*4 + 4 + 4
 CFG5_BYTES_PER_NODE_ROUND = 208  # 16*4 + 16*8 + 16
 CFG3_FLOP_PER_NODE_ROUND = 128   # 2*64
+# MI355X VALU issue peak: 1024 SIMD-32 units, one wave64 32-bit instruction per 2 cycles each at
+# 2.4 GHz (MI355X_MICROARCH.md, chip-level parameters and the per-instruction cycle table)
+VALU_PEAK_WAVE_INSTR_PER_S = 1024 * 2.4e9 / 2
 GOLDEN = os.path.join(ROOT, "tests", "golden", "fullsize.json")
 
 
@@ -129,6 +132,22 @@ def src_sha256() -> str:
         with open(os.path.join(csrc, f), "rb") as fh:
             h.update(f.encode() + b"\0" + fh.read())
     return h.hexdigest()
+
+
+def load_pmc_cfg3(kernel: str):
+    """cfg3's VALU counters (profiles/pmc_cfg3.json, tools/pmc_cfg3.sh + pmc_cfg3_json.py) for the
+    given batched kernel, if they were taken on these kernel sources (same src_sha256 / lib sha256),
+    else None."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_cfg3.json")))
+    except Exception:
+        return None
+    if d.get("src_sha256") != src_sha256() and d.get("lib_sha256") != lib_sha256():
+        return None
+    for name, m in d.get("kernels", {}).items():
+        if kernel and kernel.split("<")[0] in name and (("<2" in kernel) == ("<2" in name)):
+            return m
+    return None
 
 
 def load_pmc(kernel: str, n_nodes: int, dtype: str = "f64"):
@@ -231,6 +250,21 @@ def leg_cfg3(ctx: Ctx, reps: int = 4) -> dict:
     digest = combine_digests(all_dig)
     kmax = max(p[3] for p in parts) / 1e3
     flops = CFG3_FLOP_PER_NODE_ROUND * node_rounds
+    # cfg3's true bound is integer VALU (Philox).  VALU wave-instructions per node-round
+    # from the committed counters (taken on these sources), times this leg's node-rounds, over the
+    # leg's own HIP-event kernel time, against the VALU issue peak per GPU
+    pmc = load_pmc_cfg3(kname)
+    valu = None
+    if pmc and kmax > 0:
+        ach = pmc["valu_insts_per_node_round"] * node_rounds / kmax / ctx.world
+        valu = {"bound": "valu", "unit": "VALU wave-instr/s per GPU", "achieved": ach,
+                "peak": VALU_PEAK_WAVE_INSTR_PER_S, "frac": ach / VALU_PEAK_WAVE_INSTR_PER_S,
+                "valu_insts_per_node_round": pmc["valu_insts_per_node_round"],
+                "busy_frac_pmc": pmc.get("valu_busy_frac"),
+                "int64_share": pmc.get("SQ_INSTS_VALU_INT64", 0.0) / pmc["SQ_INSTS_VALU"],
+                "counters": "profiles/pmc_cfg3.json (rocprofv3 --pmc, keyed by kernel-source sha256); "
+                            "busy_frac_pmc = SQ_ACTIVE_INST_VALU x 4 / (SIMDs x dispatch cycles), which "
+                            "also counts the multi-cycle 64-bit multiplies and fp64 adds"}
     return {"workload": f"cfg3: 1e5 instances x 64 nodes, complete graph, p=0.2, AVERAGE, eps=1e-6 "
                         f"(SURVEY §A.10), sharded by global instance blocks; the batch run {reps} times "
                         f"back to back (one handle each) inside the timed region",
@@ -241,6 +275,7 @@ def leg_cfg3(ctx: Ctx, reps: int = 4) -> dict:
             "kernel": kname, "kernel_ms_max_rank": kmax * 1e3,
             "fp64_tflops_kernel": flops / kmax / 1e12 if kmax > 0 else None,
             "fp64_frac_of_peak": flops / kmax / 1e12 / FP64_PEAK_TFLOPS / ctx.world if kmax > 0 else None,
+            "roofline": valu,
             "instances_digest": digest,
             "golden_match": bool(g) and all(p[4] for p in parts) and digest == g.get("instances_digest") and
                             hashlib.sha256(all_rounds.astype("<u4").tobytes()).hexdigest() == g.get("rounds_sha256")}

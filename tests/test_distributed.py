@@ -58,7 +58,9 @@ def test_rendezvous_group_torch_free(tmp_path, oracle_mod, world):
     sum, and the sharded run's statistics reduction over plain sockets, launched by
     torch.distributed.run like the driver's N > 1 bench; the workers never import torch."""
     out = tmp_path / "verdict.json"
-    env = dict(os.environ, OMP_NUM_THREADS="1")
+    # the rendezvous listens on its own port (not MASTER_PORT + 1, which nothing reserved)
+    env = dict(os.environ, OMP_NUM_THREADS="1", ACSIM_RDZV_PORT=str(free_port()),
+               ACSIM_RDZV_TOKEN="test-token")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            os.path.join(HERE, "rdzv_worker.py"), str(out)]
@@ -75,6 +77,44 @@ def test_rendezvous_group_torch_free(tmp_path, oracle_mod, world):
     assert v["node_rounds"] == v["ref_node_rounds"]
     assert v["max_over_ranks"] == world - 1
     assert not v["torch_imported"]
+
+
+def test_rendezvous_rejects_oversized_message_and_bad_token():
+    """Hardening (acsim/rendezvous.py): rank 0 refuses a message above the size cap and a hello
+    whose token differs, with a ConnectionError instead of allocating or admitting it."""
+    import struct
+    import threading
+    import time
+    from acsim import rendezvous as R
+
+    def serve(port, token, errs):
+        try:
+            R.Group(0, 2, "127.0.0.1", port, timeout=20.0, token=token).close()
+        except ConnectionError as e:
+            errs.append(str(e))
+
+    # a client announcing a message above the cap
+    port, errs = free_port(), []
+    t = threading.Thread(target=serve, args=(port, "good", errs))
+    t.start()
+    for _ in range(400):
+        try:
+            c = socket.create_connection(("127.0.0.1", port), timeout=5.0)
+            break
+        except OSError:
+            time.sleep(0.05)
+    c.sendall(struct.pack("<Q", R._MAX_MSG + 1))
+    t.join(30)
+    c.close()
+    assert errs and "exceeds" in errs[0]
+    # a rank whose token differs
+    port, errs = free_port(), []
+    t = threading.Thread(target=serve, args=(port, "good", errs))
+    t.start()
+    g = R.Group(1, 2, "127.0.0.1", port, timeout=20.0, token="bad")
+    t.join(30)
+    g.close()
+    assert errs and "unexpected hello" in errs[0]
 
 
 def test_rendezvous_single_rank_is_local():

@@ -314,6 +314,52 @@ def test_deferred_finalize_matches_standalone(oracle_mod, term):
             assert np.array_equal(got, want), key
 
 
+def _pub_variant(variant):
+    """(config, csr, env, kernel-name fragment) of one phase-B family that writes the block partials
+    of an EPS binned round, and so must also publish into the verdict slots (round_binned.hip)."""
+    base = dict(topology="regular", degree=32, rule="trimmed", trim=5, eps=1e-9, max_rounds=60,
+                seed=31, trace_spread=True)
+    if variant == "split2":
+        return Config(n_nodes=40000, **base), None, dict(ACSIM_BIN_SA=2048, ACSIM_BIN_SPLIT=2), " split2"
+    if variant == "order_free":
+        return Config(n_nodes=40000, **base), None, dict(ACSIM_BIN_SA=2048, ACSIM_BIN_OF=1), "k_bin_gather_of"
+    if variant == "fixup":
+        cfg = Config(n_nodes=40000, fault_model="byzantine", n_faulty=300, byz_strategy="random",
+                     byz_delta=0.1, loss_p=0.05, **base)
+        return cfg, None, dict(ACSIM_BIN_SA=2048), "k_bin_fixup"
+    from acsim.graphs import skewed_csr
+    rowptr, colidx = skewed_csr(20000, 11, 32, 5)
+    cfg = Config(n_nodes=20000, topology="csr", rule="trimmed", trim=5, eps=1e-9, max_rounds=60, seed=31,
+                 trace_spread=True)
+    return cfg, (rowptr, colidx), dict(ACSIM_BIN_SA=1024), "k_bin"
+
+
+@pytest.mark.parametrize("variant", ["split2", "order_free", "fixup", "var"])
+def test_eps_publication_in_every_gather_variant(oracle_mod, variant):
+    """Every phase-B kernel that writes a binned round's partials publishes its (min, max) for the
+    next phase A's other workgroups (ACSIM_EPS_PUB): the two-pass, order-free,
+    fault fix-up and variable-degree (CSR) gathers, with publication on and off, across round(k)
+    calls that end mid-chunk, bit for bit against the oracle."""
+    cfg, csr, envs, frag = _pub_variant(variant)
+    got = {}
+    for pub in (1, 0):
+        with env(ACSIM_EPS_PUB=pub, **envs):
+            with acsim.Simulator(cfg, device=0, csr=csr) as g:
+                assert frag in g.kernel_name(), g.kernel_name()
+                g.round(3)
+                g.round(17)
+                g.run()
+                got[pub] = (g.rounds(), bits(g.values(0)), bits(g.spread_trace(0)))
+    kw = dict(csr=csr) if csr is not None else {}
+    with oracle_mod.OracleSimulator(cfg, threads=8, **kw) as o:
+        o.run()
+        ref = (o.rounds(), bits(o.values(0)), bits(o.spread_trace(0)))
+    assert 0 < int(ref[0][0]) < cfg.max_rounds   # converged under EPS, so the verdict decided the stop
+    for pub, got3 in got.items():
+        for a_, b_ in zip(got3, ref):
+            assert np.array_equal(a_, b_), pub
+
+
 SPLIT_CASES = ["d32_t5_eps_n50000_sa1024", "d16_t5_fixed_odd_sa512", "d8_t2_midpoint_sa256",
                "d32_t5_dlpsw_sa2048", "cfg4_shape_2e17"]
 
