@@ -1074,7 +1074,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         auto try_plan = [&](BinnedPlan& plan, const uint32_t* ell, uint64_t nr) -> hipError_t {
             if (!s->binned || bin_refused || !nr) return hipSuccess;
             hipError_t e = binned_build(plan, ell, s->N, nr, s->d, s->dp, bin_sa, tagged, s->f32, bin_of, s->stream,
-                                        false, s->status);
+                                        false, s->status, s->clean);
             if (e == hipErrorNotSupported) {
                 bin_refused = true;
                 return hipSuccess;
@@ -1105,6 +1105,9 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
             // NP-pass phase B (slot-dependent configs: fp64, two passes only; see launch_round_binned)
             if (s->bin.split > 1 && (s->clean || (!s->f32 && s->bin.split == 2)))
                 s->kname += " split" + std::to_string(s->bin.split);
+            if (s->bin.ofree) s->kname += " orderfree";
+            if (s->bin.pkA || s->bin.pkinv)   // 14-bit packed index streams
+                s->kname += std::string(" pk14") + (s->bin.pkA ? "A" : "") + (s->bin.pkinv ? "B" : "");
             if (s->bin.fix) {   // fault fix-up list instead of tagged senders
                 const size_t pos = s->kname.find("+k_bin_tag");
                 if (pos != std::string::npos) s->kname.replace(pos, 10, "+k_bin_fixup");

@@ -12,15 +12,24 @@ constexpr uint32_t kBinA = 512;        // phase-A / phase-M workgroup: 8 waves
 constexpr uint32_t kBinMCap = 19456;   // phase-M LDS image capacity (elements, 152 KiB)
 // cache-policy switches of the exchange (launch argument `pol`; ACSIM_BIN_POL overrides the default)
 constexpr uint32_t kPolNtRuns = 1;     // phase B: stage runs by nontemporal LDS-DMA
-constexpr uint32_t kPolNtStore = 2;    // phase A / M: nontemporal stage stores
+constexpr uint32_t kPolNtStore = 2;    // phase A: nontemporal stage stores
 constexpr uint32_t kPolNtInv = 4;      // phase B: nontemporal invpos loads
 constexpr uint32_t kPolRevB = 8;       // phase B: each XCD walks its receiver-block range downwards
                                        // (the stage tiles phase A wrote last are read first)
 constexpr uint32_t kPolNoPf = 16;       // phase B (NP > 1): per-part descriptor loads instead of the prefetch
 constexpr uint32_t kPolBfPick = 32;     // phase B (NP > 1): branch-free pick-up (clamped read + select)
-constexpr uint32_t kPolSc1Store = 64;   // phase A / M: write-through (sc1) stage stores instead of nt: no
+constexpr uint32_t kPolSc1Store = 64;   // phase A: write-through (sc1) stage stores instead of nt: no
                                         // dirty stage lines left in L2 for the kernel boundary to write back
-constexpr uint32_t kPolDefault = kPolNtStore | kPolNtInv | kPolBfPick;   // measured (cfg4): phase B 80 -> 71 (nt) -> 63.2 us (pick-up), phase A -1 us
+constexpr uint32_t kPolNtStoreM = 128;  // phase M (two-level plans): nontemporal stage-2 stores
+constexpr uint32_t kPolSc1StoreM = 256; // phase M: write-through (sc1) stage-2 stores
+constexpr uint32_t kPolSc1X = 512;      // phase B: write-through (sc1) stores of x^{r+1}
+// Default switches (the stage-store bits are chosen per plan).  Until round 4 the
+// stream's store flavour was a runtime argument, and the compiler merged the nontemporal and the
+// plain store of its two branches into one plain store: every "nontemporal stage store" measured
+// in rounds 1-3 was a plain store.  Made explicit (bin_stream_t<SMODE>), real nontemporal stage
+// stores cost cfg4 about 25 us per round (phase A), so one-level plans store plain.
+constexpr uint32_t kPolTwoLevelStores = 0;   // two-level plans' stage stores (cfg5): see DESIGN.md §5.8
+constexpr uint32_t kPolDefault = kPolNtInv | kPolBfPick;   // measured (cfg4): phase B 80 -> 71 (nt invpos) -> 63.2 us (pick-up)
 
 // ------------------------------------------------------------------------------ shared pieces
 // Stream [p0, p1) of an index stream: out[p] = lds[idx[p]].  Super-steps of 512 positions per
@@ -97,6 +106,9 @@ __device__ __forceinline__ void bin_stream_t(const VT* lx, const uint16_t* __res
                 out + p0, 0, (int)((p1 - p0) * sizeof(VT) < 0x7FFFFFF0ull ? (p1 - p0) * sizeof(VT) : 0x7FFFFFF0ull),
                 0x00020000);
         const uint32_t ob = (w * 256 + lane) * (uint32_t)sizeof(V2);   // this lane's byte offset in a super-step
+        // (rolled: with the store flavour a template parameter the body got small enough for the
+        // compiler to unroll it, which measured like SB = 2..4 below: ~10 us slower on cfg4)
+#pragma unroll 1
         for (uint64_t bi = 0; bi < nb; ++bi) {
             // next batch's indices (the last batch re-reads itself: no branch around the loads)
             const uint64_t bn = bi + 1 < nb ? bi + 1 : bi;
@@ -144,6 +156,114 @@ __device__ __forceinline__ void bin_stream(const VT* lx, const uint16_t* __restr
     else
         bin_stream_t<0>(lx, idx, out, p0, p1);
 }
+
+// ------------------------------------------------------------------------------ packed phase-A indices
+// 14-bit packed idxA (fp64 plans, source blocks of at most 16384 senders): the
+// stream is cut into blocks of 512 positions (one wave's super-step); block m holds lane l's eight
+// indices — positions 512m + 2(64q + l) + e, index k = 2q + e at bits [14k, 14k + 14) of a 112-bit
+// word — in three u32 planes (words m*224 + 64j + l, j = 0..2: bits 0-95) and one u16 plane
+// (u16 element m*448 + 384 + l: bits 96-111).  896 B per 512 positions instead of 1024.
+constexpr uint32_t kPk14Words = 224;   // u32 words per 512-position block
+
+__device__ __forceinline__ uint32_t pk14_extract(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t h, int k) {
+    switch (k) {   // k is a compile-time constant at every call site: one or two VALU each
+        case 0: return w0 & 0x3FFFu;
+        case 1: return (w0 >> 14) & 0x3FFFu;
+        case 2: return __builtin_amdgcn_alignbit(w1, w0, 28) & 0x3FFFu;
+        case 3: return (w1 >> 10) & 0x3FFFu;
+        case 4: return __builtin_amdgcn_alignbit(w2, w1, 24) & 0x3FFFu;
+        case 5: return (w2 >> 6) & 0x3FFFu;
+        case 6: return __builtin_amdgcn_alignbit(h, w2, 20) & 0x3FFFu;
+        default: return (h >> 2) & 0x3FFFu;
+    }
+}
+
+// random access (head / tail positions of a range)
+__device__ __forceinline__ uint32_t pk14_at(const uint32_t* __restrict__ pk, uint64_t p) {
+    const uint64_t m = p >> 9;
+    const uint32_t j = (uint32_t)p & 511u, q = j >> 7, l = (j & 127u) >> 1, e = j & 1u;
+    const uint32_t* b = pk + m * kPk14Words;
+    const uint32_t w0 = b[l], w1 = b[64 + l], w2 = b[128 + l];
+    const uint32_t h = reinterpret_cast<const uint16_t*>(pk)[m * (2 * kPk14Words) + 384 + l];
+    const uint32_t k = 2 * q + e;
+    const uint32_t bit = 14 * k, wi = bit >> 5, sh = bit & 31;
+    const uint32_t ws[4] = {w0, w1, w2, h};
+    const uint64_t two = (uint64_t)ws[wi] | (wi < 3 ? (uint64_t)ws[wi + 1] << 32 : 0ull);
+    return (uint32_t)(two >> sh) & 0x3FFFu;
+}
+
+// Stream [p0, p1) with packed indices: out[p] = lx[idx(p)].  Whole 512-position blocks go to the
+// waves in turn (wave w takes blocks mb + w, mb + w + NW, ...), software-pipelined like
+// bin_stream_t (the next block's four index loads are issued before this block's gathers and
+// stores); the partial blocks at the ends go position by position.
+template <uint32_t SMODE>
+__device__ __forceinline__ void bin_stream_pk14_t(const double* lx, const uint32_t* __restrict__ pk,
+                                                  double* __restrict__ out, uint64_t p0, uint64_t p1) {
+    constexpr uint32_t NW = kBinA / 64;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t mb = (p0 + 511) >> 9, me = p1 >> 9;
+    if (mb < me) {
+        const uint64_t nbw = (me - mb > w) ? (me - mb - w + NW - 1) / NW : 0;   // this wave's blocks
+        const uint16_t* pk16 = reinterpret_cast<const uint16_t*>(pk);
+        double2* o2 = reinterpret_cast<double2*>(out);
+        uint64_t m = mb + w;
+        uint32_t c0 = 0, c1 = 0, c2 = 0, ch = 0;
+        if (nbw) {
+            const uint32_t* b = pk + m * kPk14Words + lane;
+            c0 = __builtin_nontemporal_load(b);
+            c1 = __builtin_nontemporal_load(b + 64);
+            c2 = __builtin_nontemporal_load(b + 128);
+            ch = __builtin_nontemporal_load(pk16 + m * (2 * kPk14Words) + 384 + lane);
+        }
+#pragma unroll 1
+        for (uint64_t i = 0; i < nbw; ++i, m += NW) {
+            const uint64_t mn = i + 1 < nbw ? m + NW : m;   // the last block re-reads itself
+            const uint32_t* bn = pk + mn * kPk14Words + lane;
+            const uint32_t n0 = __builtin_nontemporal_load(bn);
+            const uint32_t n1 = __builtin_nontemporal_load(bn + 64);
+            const uint32_t n2 = __builtin_nontemporal_load(bn + 128);
+            const uint32_t nh = __builtin_nontemporal_load(pk16 + mn * (2 * kPk14Words) + 384 + lane);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const double2 v = make_double2(lx[pk14_extract(c0, c1, c2, ch, 2 * q)],
+                                               lx[pk14_extract(c0, c1, c2, ch, 2 * q + 1)]);
+                const uint64_t vi = m * 256 + q * 64 + lane;   // double2 index of positions 2vi, 2vi + 1
+                if constexpr (SMODE == 2) {
+                    // (buffer offsets are 32-bit: the descriptor is re-based per 2 GiB of stage)
+                    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+                        o2 + (vi & ~((1ull << 27) - 1)), 0, 0x7FFFFFF0, 0x00020000);
+                    bin_store_sc1(rb, (uint32_t)(vi & ((1ull << 27) - 1)) * 16u, v);
+                } else {
+                    bin_store(o2 + vi, v, SMODE == 1);
+                }
+            }
+            c0 = n0;
+            c1 = n1;
+            c2 = n2;
+            ch = nh;
+        }
+    }
+    // partial blocks at both ends (or the whole range when it holds no full block)
+    const uint64_t h1 = mb < me ? (mb << 9) : p1;
+    for (uint64_t q = p0 + threadIdx.x; q < h1; q += blockDim.x) out[q] = lx[pk14_at(pk, q)];
+    if (mb < me)
+        for (uint64_t q = (me << 9) + threadIdx.x; q < p1; q += blockDim.x) out[q] = lx[pk14_at(pk, q)];
+}
+
+__device__ __forceinline__ void bin_stream_pk14(const double* lx, const uint32_t* __restrict__ pk, double* __restrict__ out,
+                                                uint64_t p0, uint64_t p1, uint32_t smode) {
+    if (smode == 1)
+        bin_stream_pk14_t<1>(lx, pk, out, p0, p1);
+    else if (smode == 2)
+        bin_stream_pk14_t<2>(lx, pk, out, p0, p1);
+    else
+        bin_stream_pk14_t<0>(lx, pk, out, p0, p1);
+}
+
+// 14-bit packed phase-B positions (clean fp64 d = 32 plans): per receiver block b, 14 words per lane:
+// words 0-11 as three uint4 planes [b][j][256 lanes], words 12-13 as one uint2 plane [b][256]; slot t's
+// position at bits [14t, 14t + 14) of the lane's 448 bits.  14 KiB per block instead of 16.
+constexpr uint32_t kPk14InvWords = 14 * kBinSB;   // u32 words per receiver block
 
 // Copy runs [r0, r1) of a run table (start in `src` elements, element offset `pre` in the LDS
 // image; run k ends where run k+1's image begins) into LDS by 16-byte LDS-DMA.  Every run is

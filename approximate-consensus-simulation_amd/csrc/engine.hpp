@@ -171,8 +171,10 @@ struct BinnedPlan {
     uint64_t E = 0;                     // deliveries = local rows * D
     uint64_t Ep1 = 0, Ep2 = 0;          // padded stage lengths
     uint16_t* idxA = nullptr;           // [Ep1] sender index within its source block (0 in pads)
+    uint32_t* pkA = nullptr;            // idxA packed to 14 bits (binned_dev.hpp pk14; fp64, SA <= 16384), idxA then freed
     uint16_t* idxM = nullptr;           // [Ep2] position inside the phase-M LDS image (two levels)
     uint16_t* invpos = nullptr;         // [Q][D/8][kBinSB][8]: position of (receiver, slot) in block b's runs
+    uint32_t* pkinv = nullptr;          // invpos packed to 14 bits (clean fp64 d = 32 two-pass plans; binned_dev.hpp)
     uint2* tiles = nullptr;             // [Q][nrun+1] (stage start | pad count, element offset in block b's runs)
     bool ofree = false;                 // order-free phase B (rid, no invpos)
     bool var = false;                   // CSR rows below the compiled degree (kEllNone columns)
@@ -201,7 +203,7 @@ uint32_t binned_levels(uint64_t N, uint64_t NR, uint32_t d, uint32_t sa, uint32_
 // config under a sort-based rule (order-free phase B: rid instead of invpos).
 hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t NR, uint32_t d, uint32_t dp,
                         uint32_t sa, bool tagged, bool f32, bool ofree, hipStream_t s, bool var = false,
-                        const uint32_t* status = nullptr);
+                        const uint32_t* status = nullptr, bool clean = false);
 void binned_free(BinnedPlan& p);
 // clean: no slot-dependent decision (selects the plain phase-B instantiation)
 // fin: the previous round's finalize, deferred into this round's phase A (nullptr: none pending)

@@ -47,7 +47,8 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
                                                      const InstState* __restrict__ st, uint64_t N, uint32_t SA,
                                                      uint32_t segs, uint32_t chunk, uint32_t pol,
                                                      const FinalizeArgs fin, uint32_t fin_on, const SrcSel sel,
-                                                     uint64_t* __restrict__ ts, unsigned long long* __restrict__ ereset) {
+                                                     uint64_t* __restrict__ ts, unsigned long long* __restrict__ ereset,
+                                                     const uint32_t* __restrict__ pkA) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lx_raw[];
     VT* lx = reinterpret_cast<VT*>(lx_raw);
     if (st->done) return;
@@ -127,7 +128,15 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
         __syncthreads();
     }
     const uint64_t t1 = ts ? __builtin_amdgcn_s_memrealtime() : 0;
-    bin_stream(lx, idxA, stage, p0, p1, (pol & kPolSc1Store) ? 2u : (pol & kPolNtStore) ? 1u : 0u);
+    const uint32_t smode = (pol & kPolSc1Store) ? 2u : (pol & kPolNtStore) ? 1u : 0u;
+    if constexpr (sizeof(VT) == 8) {
+        if (pkA) {   // 14-bit packed indices
+            bin_stream_pk14(lx, pkA, stage, p0, p1, smode);
+            if (ts) bin_ts(ts, t0, t1);
+            return;
+        }
+    }
+    bin_stream(lx, idxA, stage, p0, p1, smode);
     if (ts) bin_ts(ts, t0, t1);
 }
 
@@ -148,7 +157,7 @@ __global__ __launch_bounds__(kBinA) void k_bin_regroup(const VT* __restrict__ st
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     bin_dma_runs(mt + (uint64_t)g * (PK + 1), w * PK / NW, (w + 1) * PK / NW, stage1, lm);
     __syncthreads();
-    bin_stream(lm, idxM, stage2, moff[g], moff[g + 1], (pol & kPolSc1Store) ? 2u : (pol & kPolNtStore) ? 1u : 0u);
+    bin_stream(lm, idxM, stage2, moff[g], moff[g + 1], (pol & kPolSc1StoreM) ? 2u : (pol & kPolNtStoreM) ? 1u : 0u);
 }
 
 // ------------------------------------------------------------------------------ phase B
@@ -231,13 +240,16 @@ __global__ __launch_bounds__(256) void k_bin_fixup(const uint4* __restrict__ fix
 // delivery (k_bin_fixup), a missing one as a quiet NaN; phase B draws the §A.5 drop mask, turns
 // dropped and NaN entries into missing ones and applies the receiver's own status — no tag
 // decoding, no Byzantine draws, clean-kernel registers.
+// PK14 (clean d = 32 plans): `invpos` points at the 14-bit packed positions
+// (binned_dev.hpp pk14inv layout) instead of the u16 table.
 template <int D, int T, bool WMSR = false, bool FAULTY = false, typename VT = double, int NP = 1, bool VAR = false,
-          bool FIX = false>
+          bool FIX = false, bool PK14 = false>
 __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) : FIX && NP > 1 && (T || WMSR) ? 4 : 1) void k_bin_gather(const RoundArgs a, const VT* __restrict__ stage,
                                                        const uint16_t* __restrict__ invpos,
                                                        const uint2* __restrict__ tiles, uint32_t nrun, uint32_t Q,
                                                        uint32_t Qc, uint32_t pol) {
     static_assert(D % 8 == 0, "invpos is read 8 slots at a time");
+    static_assert(!PK14 || (D == 32 && !FAULTY && !FIX && !VAR), "packed positions: clean d = 32 plans");
     static_assert(!(FIX && FAULTY), "FIX replaces the tagged resolution");
     constexpr bool FLT = FAULTY || FIX;   // a fault schedule or loss: receiver status and drop mask
     // runs are padded to 16-byte multiples; nrun <= D*kBinSB/16 (checked when the plan is built)
@@ -324,8 +336,39 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
         }
     }
     uint4 ip[D / 8];
+    uint32_t pw[PK14 ? 14 : 1];   // packed: the lane's 32 positions at bits [14t, 14t + 14)
+    if constexpr (PK14) {
+        const uint32_t* bb = reinterpret_cast<const uint32_t*>(invpos) + (uint64_t)b * kPk14InvWords;
+        using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+        using u32x2 = unsigned int __attribute__((ext_vector_type(2)));
+        const u32x4* p4 = reinterpret_cast<const u32x4*>(bb) + threadIdx.x;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const u32x4 t4 = __builtin_nontemporal_load(p4 + j * kBinSB);
+            pw[4 * j] = t4.x;
+            pw[4 * j + 1] = t4.y;
+            pw[4 * j + 2] = t4.z;
+            pw[4 * j + 3] = t4.w;
+        }
+        const u32x2 t2 = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(bb + 3 * 4 * kBinSB) + threadIdx.x);
+        pw[12] = t2.x;
+        pw[13] = t2.y;
+    }
+    // position of slot t (compile-time t)
+    auto pos_of = [&](int t) -> uint32_t {
+        if constexpr (PK14) {
+            const int bit = 14 * t, wi = bit >> 5, sh = bit & 31;
+            if (sh + 14 <= 32) return __builtin_amdgcn_ubfe(pw[wi], sh, 14);
+            return __builtin_amdgcn_alignbit(pw[wi + 1], pw[wi], sh) & 0x3FFFu;
+        } else {
+            const uint4& u = ip[t / 8];
+            const uint32_t wd = (t & 6) == 0 ? u.x : (t & 6) == 2 ? u.y : (t & 6) == 4 ? u.z : u.w;
+            return (t & 1) ? wd >> 16 : wd & 0xFFFFu;
+        }
+    };
     const uint4* ipp = reinterpret_cast<const uint4*>(invpos) + (uint64_t)b * (D / 8) * kBinSB + threadIdx.x;
-    if (pol & kPolNtInv) {
+    if constexpr (PK14) {
+    } else if (pol & kPolNtInv) {
         using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
         const u32x4* ipn = reinterpret_cast<const u32x4*>(ipp);
 #pragma unroll
@@ -343,14 +386,7 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
         __syncthreads();
         if (a.ts) t1 = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
-        for (int q = 0; q < D / 8; ++q) {
-            const uint32_t wd[4] = {ip[q].x, ip[q].y, ip[q].z, ip[q].w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                v[1 + 8 * q + 2 * e] = raw[wd[e] & 0xFFFFu];
-                v[2 + 8 * q + 2 * e] = raw[wd[e] >> 16];
-            }
-        }
+        for (int t = 0; t < D; ++t) v[1 + t] = raw[pos_of(t)];
     } else {
 #pragma unroll
         // Unrolled: the first part skips the p >= lo test and the last part the p < hi test.  This
@@ -378,10 +414,9 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
             if (k == 0 && a.ts) t1 = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
             for (int q = 0; q < D / 8; ++q) {
-                const uint32_t wd[4] = {ip[q].x, ip[q].y, ip[q].z, ip[q].w};
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const uint32_t p0 = wd[e] & 0xFFFFu, p1 = wd[e] >> 16;
+                    const uint32_t p0 = pos_of(8 * q + 2 * e), p1 = pos_of(8 * q + 2 * e + 1);
                     const bool in0 = (k == 0 || p0 >= lo) && (k + 1 == (uint32_t)NP || p0 < hi);
                     const bool in1 = (k == 0 || p1 >= lo) && (k + 1 == (uint32_t)NP || p1 < hi);
                     // (faulty kernels: exec-masked reads straight into v; the clamped read + select
@@ -477,7 +512,20 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
             else
                 res = apply_rule_reg<D, T, WMSR>(a.rule, v);
         }
-        reinterpret_cast<VT*>(a.xout)[i] = res;
+        if (pol & kPolSc1X) {   // write-through: no dirty x lines left in L2 at the kernel boundary
+            const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+                reinterpret_cast<VT*>(a.xout) + (i - threadIdx.x), 0, (int)(kBinSB * sizeof(VT)), 0x00020000);
+            if constexpr (sizeof(VT) == 8) {
+                using UV = unsigned int __attribute__((ext_vector_type(2)));
+                UV bits;
+                __builtin_memcpy(&bits, &res, 8);
+                __builtin_amdgcn_raw_buffer_store_b64(bits, rx, threadIdx.x * 8u, 0, 16);
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, res), rx, threadIdx.x * 4u, 0, 16);
+            }
+        } else {
+            reinterpret_cast<VT*>(a.xout)[i] = res;
+        }
         if (si == kHonest) {
             mn = res;
             mx = res;
@@ -715,6 +763,51 @@ __global__ __launch_bounds__(256) void k_bin_fill_a(const uint32_t* __restrict__
     idxA[pstart[key] + (p - tl[key].x)] = (uint16_t)(ell_at(ell, e / G.D, e % G.D, G.dp) % G.SA);
 }
 
+// idxA -> 14-bit packed blocks (binned_dev.hpp pk14): one thread per (512-position block m, lane l)
+__global__ __launch_bounds__(256) void k_bin_pack14(const uint16_t* __restrict__ idx, uint64_t n, uint32_t* __restrict__ pk) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t m = t >> 6;
+    const uint32_t l = (uint32_t)t & 63u;
+    if (m * 512 >= n) return;
+    uint64_t acc[2] = {0ull, 0ull};   // bits 0-63, 64-127
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint64_t pos = m * 512 + 2 * (64 * (uint64_t)(k >> 1) + l) + (k & 1);
+        const uint64_t v = pos < n ? (uint64_t)(idx[pos] & 0x3FFFu) : 0ull;
+        const int bit = 14 * k;
+        if (bit < 64) {
+            acc[0] |= v << bit;
+            if (bit + 14 > 64) acc[1] |= v >> (64 - bit);
+        } else {
+            acc[1] |= v << (bit - 64);
+        }
+    }
+    uint32_t* b = pk + m * kPk14Words + l;
+    b[0] = (uint32_t)acc[0];
+    b[64] = (uint32_t)(acc[0] >> 32);
+    b[128] = (uint32_t)acc[1];
+    reinterpret_cast<uint16_t*>(pk)[m * (2 * kPk14Words) + 384 + l] = (uint16_t)(acc[1] >> 32);
+}
+
+// invpos (d = 32) -> 14-bit packed positions (binned_dev.hpp kPk14InvWords layout): workgroup = block b,
+// lane = receiver
+__global__ __launch_bounds__(kBinSB) void k_bin_pack14inv(const uint16_t* __restrict__ invpos, uint32_t* __restrict__ pk) {
+    constexpr uint32_t D = 32;
+    const uint32_t b = blockIdx.x, l = threadIdx.x;
+    uint32_t w[14] = {};
+    for (uint32_t t = 0; t < D; ++t) {
+        const uint32_t v = invpos[(((uint64_t)b * (D / 8) + t / 8) * kBinSB + l) * 8 + (t & 7)] & 0x3FFFu;
+        const uint32_t bit = 14 * t, wi = bit >> 5, sh = bit & 31;
+        w[wi] |= v << sh;
+        if (sh + 14 > 32) w[wi + 1] |= v >> (32 - sh);
+    }
+    uint32_t* bb = pk + (uint64_t)b * kPk14InvWords;
+    for (uint32_t j = 0; j < 3; ++j)
+        for (uint32_t c = 0; c < 4; ++c) bb[(j * kBinSB + l) * 4 + c] = w[4 * j + c];
+    bb[3 * 4 * kBinSB + 2 * l] = w[12];
+    bb[3 * 4 * kBinSB + 2 * l + 1] = w[13];
+}
+
 // phase-A ranges: aoff[a] = padded start of source block a's deliveries (aoff[P] = Ep)
 __global__ __launch_bounds__(256) void k_bin_aoff(const uint32_t* __restrict__ pstart, uint32_t P, uint32_t G1,
                                                   uint64_t Ep, uint64_t* __restrict__ aoff) {
@@ -900,6 +993,8 @@ void binned_free(BinnedPlan& p) {
         (void)hipFree(p.ts);
     }
     (void)hipFree(p.idxA);
+    (void)hipFree(p.pkA);
+    (void)hipFree(p.pkinv);
     (void)hipFree(p.idxM);
     (void)hipFree(p.invpos);
     (void)hipFree(p.rid);
@@ -982,7 +1077,7 @@ hipError_t tile_sort(const uint32_t* ell, uint64_t E, const BinGeom& G, int leve
 
 hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t NR, uint32_t d, uint32_t dp,
                         uint32_t sa, bool tagged, bool f32, bool ofree, hipStream_t s, bool var,
-                        const uint32_t* status) {
+                        const uint32_t* status, bool clean) {
     if (var && (f32 || ofree)) return hipErrorNotSupported;   // CSR plans: fp64, invpos phase B
     hipError_t e = hipSuccess;
     uint32_t sr = 0;
@@ -1042,6 +1137,24 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
         hipLaunchKernelGGL(k_bin_aoff, dim3((G.P + 256) / 256), dim3(256), 0, s, T1.pstart, G.P, G.R, p.Ep1, p.aoff);
         e = hipGetLastError();
     }
+    // 14-bit packed phase-A indices (fp64 plans with source blocks of at most 2^14 senders; ACSIM_BIN_PACK=0: u16)
+    if (e == hipSuccess && !f32 && sa <= 16384) {
+        const char* v = getenv("ACSIM_BIN_PACK");
+        if (!v || strtoul(v, nullptr, 10) != 0) {
+            const uint64_t nb = (p.Ep1 + 511) / 512;
+            e = hipMalloc(&p.pkA, nb * kPk14Words * 4);
+            if (e == hipSuccess) {
+                hipLaunchKernelGGL(k_bin_pack14, dim3((unsigned)((nb * 64 + 255) / 256)), dim3(256), 0, s, p.idxA, p.Ep1,
+                                   p.pkA);
+                e = hipGetLastError();
+            }
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e == hipSuccess) {
+                (void)hipFree(p.idxA);
+                p.idxA = nullptr;
+            }
+        }
+    }
     TileSort* last = &T1;
     if (e == hipSuccess && levels == 2) {
         // ---- level 2 (phase M): PK-run images per (r, k), regrouped by receiver block
@@ -1094,7 +1207,7 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     p.ofree = ofree;
     {
         const char* v = getenv("ACSIM_BIN_POL");
-        p.pol = v ? (uint32_t)strtoul(v, nullptr, 0) & 127u : kPolDefault;
+        p.pol = v ? (uint32_t)strtoul(v, nullptr, 0) & 1023u : kPolDefault | (G.levels == 2 ? kPolTwoLevelStores : 0u);
     }
     if (ofree) {   // order-free phase B: receiver ids in image order
         p.rstride = ((uint32_t)d * kBinSB + p.nrun * (G.pad - 1) + 15u) & ~15u;
@@ -1171,6 +1284,27 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
                     fits = row[(k + 1) * p.nrun / np].y - row[k * p.nrun / np].y <= cap;
             }
             if (fits) p.split = np;
+            // 14-bit packed positions for phase B: clean fp64 d = 32 two-pass
+            // plans whose every block image holds fewer than 2^14 entries
+            uint32_t mxpos = 0;
+            for (uint32_t b = 0; b < G.Q; ++b) {
+                const uint32_t tot = h[(uint64_t)b * (p.nrun + 1) + p.nrun].y;
+                mxpos = tot > mxpos ? tot : mxpos;
+            }
+            const char* pv = getenv("ACSIM_BIN_PACK");
+            if (e == hipSuccess && p.split == 2 && clean && !tagged && !f32 && !var && D == 32 && mxpos <= 16384 &&
+                !(pv && strtoul(pv, nullptr, 10) == 0)) {
+                e = hipMalloc(&p.pkinv, (uint64_t)G.Q * kPk14InvWords * 4);
+                if (e == hipSuccess) {
+                    hipLaunchKernelGGL(k_bin_pack14inv, dim3(G.Q), dim3(kBinSB), 0, s, p.invpos, p.pkinv);
+                    e = hipGetLastError();
+                }
+                if (e == hipSuccess) e = hipStreamSynchronize(s);
+                if (e == hipSuccess) {
+                    (void)hipFree(p.invpos);
+                    p.invpos = nullptr;
+                }
+            }
         }
     }
     // phase-A segmentation: for few source blocks about 256 workgroups per launch (one generation: one 128 KiB-LDS
@@ -1239,7 +1373,12 @@ static hipError_t binned_set_lds_attributes() {
 // clean phase B in p.split (2..4) passes
 #define ACS_BIN_NP_LAUNCH(DD, TT, W, VT_, SRC)                                                         \
     {                                                                                                  \
-        if (p.split == 2)                                                                              \
+        if (p.split == 2 && p.pkinv) {                                                                 \
+            if constexpr (DD == 32 && sizeof(VT_) == 8)                                                    \
+                hipLaunchKernelGGL((k_bin_gather<DD, TT, W, false, VT_, 2, false, false, true>), grid,     \
+                                   dim3(kBinSB), 0, s, a, SRC, reinterpret_cast<const uint16_t*>(p.pkinv), \
+                                   p.tiles, p.nrun, p.Q, Qc, pol);                                        \
+        } else if (p.split == 2)                                                                       \
             hipLaunchKernelGGL((k_bin_gather<DD, TT, W, false, VT_, 2>), grid, dim3(kBinSB), 0, s, a, SRC, \
                                p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                  \
         else if (p.split == 3)                                                                         \
@@ -1280,7 +1419,8 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
         }
         if (phases & 1)
             hipLaunchKernelGGL(k_bin_scatter<float>, dim3((nsrc + 7) / 8 * 8 * p.segs), dim3(kBinA), p.SA * sizeof(float), s,
-                               fsrc, p.idxA, p.aoff, st1, a.st, a.N, p.SA, p.segs, p.chunk, pol, fa, fin_on, sel, p.ts, a.eacc);
+                               fsrc, p.idxA, p.aoff, st1, a.st, a.N, p.SA, p.segs, p.chunk, pol, fa, fin_on, sel, p.ts, a.eacc,
+                               nullptr);
         if (p.levels == 2) {
             float* st2 = reinterpret_cast<float*>(p.stage2);
             if (phases & 2)
@@ -1339,7 +1479,8 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
     }
     if (phases & 1)
         hipLaunchKernelGGL(k_bin_scatter<double>, dim3((nsrc + 7) / 8 * 8 * p.segs), dim3(kBinA), p.SA * sizeof(double), s, src,
-                           p.idxA, p.aoff, p.stage1, a.st, a.N, p.SA, p.segs, p.chunk, pol, fa, fin_on, sel, p.ts, a.eacc);
+                           p.idxA, p.aoff, p.stage1, a.st, a.N, p.SA, p.segs, p.chunk, pol, fa, fin_on, sel, p.ts, a.eacc,
+                           p.pkA);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const double* last = p.stage1;

@@ -279,10 +279,12 @@ def test_order_free_f32_and_wmsr(oracle_mod):
             assert np.array_equal(gx.view(np.uint8), o.values(0).view(np.uint8))
 
 
-@pytest.mark.parametrize("pol", [0, 1, 2, 7])
-def test_cache_policy_switches_bit_exact(oracle_mod, pol):
-    """ACSIM_BIN_POL only changes cache policies (nontemporal runs / stores / invpos loads)."""
-    cfg, sa = CASES["d32_t5_eps_n50000_sa1024"]
+@pytest.mark.parametrize("name,pol", [("d32_t5_eps_n50000_sa1024", p) for p in (0, 1, 2, 7, 64, 36)] +
+                         [("two_level_d16_t5_n100000_sa256", p) for p in (0, 2, 128, 130, 256, 322)])
+def test_cache_policy_switches_bit_exact(oracle_mod, name, pol):
+    """ACSIM_BIN_POL only changes cache policies (nontemporal runs / phase-A and phase-M stage
+    stores, plain / nontemporal / write-through, and invpos loads)."""
+    cfg, sa = CASES[name]
     with env(ACSIM_BIN_SA=sa, ACSIM_BIN_POL=pol):
         kb, rb, xb, tb = run_gpu(cfg)
     with oracle_mod.OracleSimulator(cfg, threads=8) as o:
@@ -322,7 +324,7 @@ def _pub_variant(variant):
     if variant == "split2":
         return Config(n_nodes=40000, **base), None, dict(ACSIM_BIN_SA=2048, ACSIM_BIN_SPLIT=2), " split2"
     if variant == "order_free":
-        return Config(n_nodes=40000, **base), None, dict(ACSIM_BIN_SA=2048, ACSIM_BIN_OF=1), "k_bin_gather_of"
+        return Config(n_nodes=40000, **base), None, dict(ACSIM_BIN_SA=2048, ACSIM_BIN_OF=1), " orderfree"
     if variant == "fixup":
         cfg = Config(n_nodes=40000, fault_model="byzantine", n_faulty=300, byz_strategy="random",
                      byz_delta=0.1, loss_p=0.05, **base)
