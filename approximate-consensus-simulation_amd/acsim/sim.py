@@ -193,9 +193,12 @@ class Simulator:
         return out.reshape(self.N, d)
 
     # -------------------------------------------------------------------------- measurement
-    def set_kernel_timing(self, enable, every: int = 1) -> None:
-        """Bracket round-kernel launches with HIP events (every `every`-th round when enabled)."""
-        self._chk(self._lib.acs_set_kernel_timing(self._h, max(1, int(every)) if enable else 0))
+    def set_kernel_timing(self, enable, every: int = 1, runs: bool = False) -> None:
+        """Bracket round-kernel launches with HIP events: every `every`-th round when enabled, or
+        with runs=True one event pair around each run of `every` consecutive rounds (no idle gap
+        inside the run; every round counts as one launch)."""
+        k = max(1, int(every)) if enable else 0
+        self._chk(self._lib.acs_set_kernel_timing(self._h, -k if runs else k))
 
     def kernel_timing(self):
         """(total_ms, launches, kernel_name) of the round kernel since timing was enabled."""

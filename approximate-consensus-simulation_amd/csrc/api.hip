@@ -141,6 +141,10 @@ struct acs_sim {
     std::vector<Part> parts;       // virtual partitions 1..P-1 (partition 0 uses x / ell)
     // kernel timing (bench)
     uint32_t timing = 0;           // 0 off, else bracket every timing-th round (sampling)
+    bool timing_runs = false;      // bracket runs of `timing` consecutive rounds instead (one pair each)
+    hipEvent_t run_end = nullptr;  // the open run's end event (recorded after its last round)
+    uint32_t run_rounds = 0;       // rounds in the open run
+    std::vector<uint32_t> ev_w;    // rounds covered by each event pair
     uint64_t timing_ctr = 0;
     std::vector<hipEvent_t> ev;    // pairs (start, stop)
     size_t ev_used = 0;
@@ -351,7 +355,7 @@ static int harvest_timing(acs_sim* s) {
         float ms = 0.f;
         HIP_TRY(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
         s->timed_ms += ms;
-        s->timed_launches += 1;
+        s->timed_launches += k / 2 < s->ev_w.size() ? s->ev_w[k / 2] : 1u;
     }
     s->ev_used = 0;
     return ACS_OK;
@@ -361,15 +365,51 @@ static int harvest_timing(acs_sim* s) {
 // launch covering a whole round(k) call: acs_get_kernel_timing counts launches, not rounds)
 static int timing_begin(acs_sim* s, hipEvent_t* e1) {
     *e1 = nullptr;
+    if (s->timing && s->timing_runs) {   // runs of `timing` consecutive rounds, one pair per run
+        const uint64_t pos = s->timing_ctr++ % s->timing;
+        if (pos == 0 && !s->run_end) {
+            if (s->ev_used + 2 > 4096) {
+                int rc = harvest_timing(s);
+                if (rc) return rc;
+            }
+            if (s->ev_w.size() < s->ev_used / 2 + 1) s->ev_w.resize(s->ev_used / 2 + 1);
+            s->ev_w[s->ev_used / 2] = 0;
+            hipEvent_t e0 = next_event(s);
+            s->run_end = next_event(s);
+            if (!e0 || !s->run_end) return fail(ACS_EDEVICE, "hipEventCreate failed");
+            HIP_TRY(hipEventRecord(e0, s->stream));
+            s->run_rounds = 0;
+        }
+        s->run_rounds++;
+        if (pos + 1 == s->timing) {   // the run's last round: the caller records the end event
+            *e1 = s->run_end;
+            s->ev_w[s->ev_used / 2 - 1] = s->run_rounds;
+            s->run_end = nullptr;
+        }
+        return ACS_OK;
+    }
     if (!s->timing || s->timing_ctr++ % s->timing != 0) return ACS_OK;
     if (s->ev_used + 2 > 4096) {
         int rc = harvest_timing(s);
         if (rc) return rc;
     }
+    if (s->ev_w.size() < s->ev_used / 2 + 1) s->ev_w.resize(s->ev_used / 2 + 1);
+    s->ev_w[s->ev_used / 2] = 1;
     hipEvent_t e0 = next_event(s);
     *e1 = next_event(s);
     if (!e0 || !*e1) return fail(ACS_EDEVICE, "hipEventCreate failed");
     HIP_TRY(hipEventRecord(e0, s->stream));
+    return ACS_OK;
+}
+
+// Close a timing run still open at the end of an advance() call (run mode: a run never spans
+// two calls, so host time between calls is never bracketed).
+static int timing_close(acs_sim* s) {
+    if (!s->run_end) return ACS_OK;
+    HIP_TRY(hipEventRecord(s->run_end, s->stream));
+    s->ev_w[s->ev_used / 2 - 1] = s->run_rounds;
+    s->run_end = nullptr;
+    s->timing_ctr = 0;
     return ACS_OK;
 }
 
@@ -713,6 +753,7 @@ static int advance(acs_sim* s, uint32_t k) {
         else
             HIP_TRY(launch_batched_small(a, s->B, k, s->stream));
         if (e1) HIP_TRY(hipEventRecord(e1, s->stream));
+        if (int rc2 = timing_close(s)) return rc2;   // (run mode: one launch per call)
         // The done count (and, for acs_run, the result summary) ride on the same synchronisation,
         // folded from the instances' done flags in one launch that writes host memory: no copies
         // (each costs a DMA round trip) and no per-instance atomic on one counter (the batched
@@ -764,6 +805,10 @@ static int advance(acs_sim* s, uint32_t k) {
     }
     for (hipEvent_t e : poll)
         if (e) (void)hipEventDestroy(e);
+    if (s->run_end) {   // a timing run cut short by the end of this call
+        if (int rc = flush_finalize(s)) return rc;
+        if (int rc = timing_close(s)) return rc;
+    }
     HIP_TRY(hipMemcpyAsync(s->h_ndone, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     s->all_done = s->h_ndone[0] == s->B;
@@ -1548,7 +1593,9 @@ int acs_set_kernel_timing(acs_sim* s, int enable) {
     HIP_TRY(hipSetDevice(s->device));
     int rc = harvest_timing(s);
     if (rc) return rc;
-    s->timing = enable > 0 ? (uint32_t)enable : 0u;
+    s->timing = enable > 0 ? (uint32_t)enable : enable < 0 ? (uint32_t)(-(int64_t)enable) : 0u;
+    s->timing_runs = enable < 0;
+    s->run_end = nullptr;
     s->timing_ctr = 0;
     s->timed_ms = 0.0;
     s->timed_launches = 0;

@@ -328,10 +328,12 @@ __device__ __forceinline__ VT shfl_xor_v(VT v, int m) {
 #ifndef ACS_SPLIT_WPE
 #define ACS_SPLIT_WPE 0   // variant builds: waves per SIMD asked of the fp64 F = 2 kernel (unbounded: 98 VGPRs, 4)
 #endif
-template <int F, typename VT>
-__device__ __forceinline__ void batched_split_body(const BatchArgs& a, uint32_t kmax, uint32_t lb) {
+template <int F, typename VT = double>
+__global__ __launch_bounds__(64 * F, (F == 2 && sizeof(VT) == 8 && ACS_SPLIT_WPE) ? ACS_SPLIT_WPE : 1) void k_batched_split(
+    const BatchArgs a, uint32_t kmax) {
     constexpr int R = 64 / F;        // receivers per wave
     constexpr int CPL = 16 / F;      // Philox calls (4 slots each) per lane and round
+    const uint32_t lb = blockIdx.x;
     InstState* S = a.st + lb;
     if (S->done) return;
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -406,28 +408,6 @@ __device__ __forceinline__ void batched_split_body(const BatchArgs& a, uint32_t 
     }
 }
 
-template <int F, typename VT = double>
-__global__ __launch_bounds__(64 * F, (F == 2 && sizeof(VT) == 8 && ACS_SPLIT_WPE) ? ACS_SPLIT_WPE : 1) void k_batched_split(
-    const BatchArgs a, uint32_t kmax) {
-    batched_split_body<F, VT>(a, kmax, blockIdx.x);
-}
-
-// The batch's last instances with four lanes per receiver (DESIGN.md §6, cfg3 scaling): 256-thread
-// workgroups; workgroup b < nmain runs instance b with two lanes per receiver on its first two waves
-// (the other two end at once, so the CU holds the same waves as with 128-thread workgroups), the
-// last B - nmain run theirs with four.  Dispatch is in order in practice, so the instances that
-// finish last — whose latency, not the chip's throughput, sets the end of a small shard — run at
-// 0.6x the latency for 1.26x the work.  Instances are independent: any order gives the same result.
-template <typename VT = double>
-__global__ __launch_bounds__(256) void k_batched_split_tail(const BatchArgs a, uint32_t kmax, uint32_t nmain) {
-    if (blockIdx.x < nmain) {
-        if (threadIdx.x >= 128) return;   // (an ended wave no longer counts at the barriers)
-        batched_split_body<2, VT>(a, kmax, blockIdx.x);
-    } else {
-        batched_split_body<4, VT>(a, kmax, blockIdx.x);
-    }
-}
-
 // Lanes per receiver for a clean AVERAGE batch of 64-node instances: ACSIM_BATCH_SPLIT (1, 2, 4)
 // or the default.
 uint32_t batched_split_factor(uint32_t N, uint32_t rule, bool faults) {
@@ -478,23 +458,10 @@ hipError_t launch_batched_small(const BatchArgs& a, uint64_t B, uint32_t k, hipS
     const uint32_t F = batched_split_factor(a.N, a.rule, a.status != nullptr);
     if (F > 1) {
         const dim3 grid((unsigned)B), block(64 * F);
-        // ACSIM_BATCH_LDS=<bytes>: dynamic LDS per workgroup, unused by the kernel; it caps the resident
-        // workgroups per CU (occupancy experiments)
-        const char* lv = getenv("ACSIM_BATCH_LDS");
-        const uint32_t lds = lv ? (uint32_t)strtoul(lv, nullptr, 10) : 0u;
-        // ACSIM_BATCH_TAIL=<n>: the last n instances with four lanes per receiver (k_batched_split_tail)
-        const char* tv = getenv("ACSIM_BATCH_TAIL");
-        const uint32_t tail = tv ? (uint32_t)strtoul(tv, nullptr, 10) : 0u;
-        if (F == 2 && tail) {
-            const uint32_t nmain = B > tail ? (uint32_t)(B - tail) : 0u;
-            if (a.f32) hipLaunchKernelGGL((k_batched_split_tail<float>), grid, dim3(256), lds, s, a, k, nmain);
-            else hipLaunchKernelGGL((k_batched_split_tail<double>), grid, dim3(256), lds, s, a, k, nmain);
-            return hipGetLastError();
-        }
-        if (F == 2 && a.f32) hipLaunchKernelGGL((k_batched_split<2, float>), grid, block, lds, s, a, k);
-        else if (F == 2) hipLaunchKernelGGL((k_batched_split<2, double>), grid, block, lds, s, a, k);
-        else if (a.f32) hipLaunchKernelGGL((k_batched_split<4, float>), grid, block, lds, s, a, k);
-        else hipLaunchKernelGGL((k_batched_split<4, double>), grid, block, lds, s, a, k);
+        if (F == 2 && a.f32) hipLaunchKernelGGL((k_batched_split<2, float>), grid, block, 0, s, a, k);
+        else if (F == 2) hipLaunchKernelGGL((k_batched_split<2, double>), grid, block, 0, s, a, k);
+        else if (a.f32) hipLaunchKernelGGL((k_batched_split<4, float>), grid, block, 0, s, a, k);
+        else hipLaunchKernelGGL((k_batched_split<4, double>), grid, block, 0, s, a, k);
         return hipGetLastError();
     }
     return a.f32 ? launch_batched_small_t<float>(a, B, k, s) : launch_batched_small_t<double>(a, B, k, s);

@@ -28,7 +28,12 @@ constexpr uint32_t kPolSc1X = 512;      // phase B: write-through (sc1) stores o
 // plain store of its two branches into one plain store: every "nontemporal stage store" measured
 // in rounds 1-3 was a plain store.  Made explicit (bin_stream_t<SMODE>), real nontemporal stage
 // stores cost cfg4 about 25 us per round (phase A), so one-level plans store plain.
-constexpr uint32_t kPolTwoLevelStores = 0;   // two-level plans' stage stores (cfg5): see DESIGN.md §5.8
+// stage stores by plan (DESIGN.md §5.8, A/B inside one build): one level (cfg4) write-through phase-A
+// stores, 118 against 122 us per round for plain ones (no dirty stage lines for the kernel boundary
+// to write back; nontemporal ones 137 us); two levels (cfg5) nontemporal phase-A and phase-M stores,
+// 7.60 against 7.86 ms per round for plain ones (the 16 GiB of stages far exceed the MALL)
+constexpr uint32_t kPolOneLevelStores = kPolSc1Store;
+constexpr uint32_t kPolTwoLevelStores = kPolNtStore | kPolNtStoreM;
 constexpr uint32_t kPolDefault = kPolNtInv | kPolBfPick;   // measured (cfg4): phase B 80 -> 71 (nt invpos) -> 63.2 us (pick-up)
 
 // ------------------------------------------------------------------------------ shared pieces

@@ -1137,10 +1137,12 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
         hipLaunchKernelGGL(k_bin_aoff, dim3((G.P + 256) / 256), dim3(256), 0, s, T1.pstart, G.P, G.R, p.Ep1, p.aoff);
         e = hipGetLastError();
     }
-    // 14-bit packed phase-A indices (fp64 plans with source blocks of at most 2^14 senders; ACSIM_BIN_PACK=0: u16)
+    // 14-bit packed phase-A indices (fp64 plans with source blocks of at most 2^14 senders).
+    // ACSIM_BIN_PACK: bit 0 phase A, bit 1 phase B (default 3; 0: u16 streams)
+    const char* pack_env = getenv("ACSIM_BIN_PACK");
+    const uint32_t pack = pack_env ? (uint32_t)strtoul(pack_env, nullptr, 10) : 3u;
     if (e == hipSuccess && !f32 && sa <= 16384) {
-        const char* v = getenv("ACSIM_BIN_PACK");
-        if (!v || strtoul(v, nullptr, 10) != 0) {
+        if (pack & 1u) {
             const uint64_t nb = (p.Ep1 + 511) / 512;
             e = hipMalloc(&p.pkA, nb * kPk14Words * 4);
             if (e == hipSuccess) {
@@ -1207,7 +1209,7 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     p.ofree = ofree;
     {
         const char* v = getenv("ACSIM_BIN_POL");
-        p.pol = v ? (uint32_t)strtoul(v, nullptr, 0) & 1023u : kPolDefault | (G.levels == 2 ? kPolTwoLevelStores : 0u);
+        p.pol = v ? (uint32_t)strtoul(v, nullptr, 0) & 1023u : kPolDefault | (G.levels == 2 ? kPolTwoLevelStores : kPolOneLevelStores);
     }
     if (ofree) {   // order-free phase B: receiver ids in image order
         p.rstride = ((uint32_t)d * kBinSB + p.nrun * (G.pad - 1) + 15u) & ~15u;
@@ -1291,9 +1293,8 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
                 const uint32_t tot = h[(uint64_t)b * (p.nrun + 1) + p.nrun].y;
                 mxpos = tot > mxpos ? tot : mxpos;
             }
-            const char* pv = getenv("ACSIM_BIN_PACK");
             if (e == hipSuccess && p.split == 2 && clean && !tagged && !f32 && !var && D == 32 && mxpos <= 16384 &&
-                !(pv && strtoul(pv, nullptr, 10) == 0)) {
+                (pack & 2u)) {
                 e = hipMalloc(&p.pkinv, (uint64_t)G.Q * kPk14InvWords * 4);
                 if (e == hipSuccess) {
                     hipLaunchKernelGGL(k_bin_pack14inv, dim3(G.Q), dim3(kBinSB), 0, s, p.invpos, p.pkinv);

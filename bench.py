@@ -11,11 +11,13 @@ The roofline object prices the dominant kernel at SURVEY §8(d)'s algorithmic 40
 (32·4 B column ids + 32·8 B neighbour values + 8 B own value + 8 B store) times the N nodes one
 launch processes, divided by its average device duration measured with HIP events on the
 handle's stream over the timed region.  On cfg4 the round is the binned exchange
-(csrc/round_binned.hip): two launches, k_bin_scatter then k_bin_gather, bracketed together by
-one event pair, so "one launch" here means that pair.  The ε-spread fold of the previous round runs
-inside k_bin_scatter (deferred finalize) and is therefore included; the one
-standalone k_finalize per 16-round chunk is not.  Every --event-every-th timed round (default 10)
-is bracketed: an event pair idles the stream for ~5 µs, which would otherwise inflate ms_per_step.
+(csrc/round_binned.hip): two launches, k_bin_scatter then k_bin_gather, so "one launch" here means
+that pair, i.e. one round.  The events bracket runs of --event-run consecutive timed rounds (default
+25: four runs in a 100-step region), one pair per run, so a round's device time includes the
+boundary between its two kernels and the one to the next round, and no event-induced idle (a pair
+around every 10th single round, rounds 1-3, idled the stream for ~5 µs and inflated the bracketed
+round by ~2 µs).  The ε-spread fold of the previous round runs inside k_bin_scatter (deferred
+finalize); the one standalone k_finalize per 16-round chunk falls inside a run.
 `traffic` is the pair's measured HBM bytes per round from the committed rocprofv3 PMC summary
 (profiles/pmc_cfg4.json, FETCH_SIZE x 2 + WRITE_SIZE, tools/traffic_json.py); it is reported only
 when that summary was taken on this build (same library sha256, or the same sha256 of the kernel
@@ -60,9 +62,9 @@ BYTES_PER_NODE_ROUND = 400  # 32*4 + 32*8 + 8 + 8
 BYTES_PER_NODE_ROUND_F32 = 264  # SURVEY §8(d) fp32 mode: 32*4 + 32*4 + 4 + 4
 CFG5_BYTES_PER_NODE_ROUND = 208  # 16*4 + 16*8 + 16
 CFG3_FLOP_PER_NODE_ROUND = 128   # 2*64
-# MI355X VALU issue peak: 1024 SIMD-32 units, one wave64 32-bit instruction per 2 cycles each at
-# 2.4 GHz (MI355X_MICROARCH.md, chip-level parameters and the per-instruction cycle table)
-VALU_PEAK_WAVE_INSTR_PER_S = 1024 * 2.4e9 / 2
+# MI355X VALU capacity: 1024 SIMDs x 2.4 GHz SIMD-cycles/s (MI355X_MICROARCH.md chip-level parameters);
+# SQ_ACTIVE_INST_VALU counts quad-cycles, so x 4 gives the SIMD-cycles the VALU pipe was busy
+VALU_PEAK_SIMD_CYCLES_PER_S = 1024 * 2.4e9
 GOLDEN = os.path.join(ROOT, "tests", "golden", "fullsize.json")
 
 
@@ -79,9 +81,9 @@ def parse():
                    help="target CPU work for the bounded cpu_baseline sample")
     p.add_argument("--no-event-timing", action="store_true",
                    help="skip per-launch HIP events (roofline then uses ms_per_step)")
-    p.add_argument("--event-every", type=int, default=10,
-                   help="bracket every k-th timed round with HIP events (each pair idles the "
-                        "stream ~5 us, so sampling keeps the timed region representative)")
+    p.add_argument("--event-run", type=int, default=25,
+                   help="bracket runs of k consecutive timed rounds with one HIP event pair each "
+                        "(per-round device time with no event-induced idle inside a run)")
     p.add_argument("--legs", default="f32,cfg3,cfg5",
                    help="comma-separated extra legs (f32, cfg3, cfg5); empty for none")
     p.add_argument("--leg-timeout", type=float, default=180.0,
@@ -256,15 +258,20 @@ def leg_cfg3(ctx: Ctx, reps: int = 4) -> dict:
     pmc = load_pmc_cfg3(kname)
     valu = None
     if pmc and kmax > 0:
-        ach = pmc["valu_insts_per_node_round"] * node_rounds / kmax / ctx.world
-        valu = {"bound": "valu", "unit": "VALU wave-instr/s per GPU", "achieved": ach,
-                "peak": VALU_PEAK_WAVE_INSTR_PER_S, "frac": ach / VALU_PEAK_WAVE_INSTR_PER_S,
-                "valu_insts_per_node_round": pmc["valu_insts_per_node_round"],
+        nr = pmc["node_rounds_per_launch"]
+        busy_per_nr = pmc["SQ_ACTIVE_INST_VALU"] * 4 / nr
+        ach = busy_per_nr * node_rounds / kmax / ctx.world
+        valu = {"bound": "valu", "unit": "VALU busy SIMD-cycles/s per GPU", "achieved": ach,
+                "peak": VALU_PEAK_SIMD_CYCLES_PER_S, "frac": ach / VALU_PEAK_SIMD_CYCLES_PER_S,
+                "valu_busy_cycles_per_node_round": busy_per_nr,
+                "valu_insts_per_node_round": pmc["SQ_INSTS_VALU"] / nr,
+                "valu_insts_per_s": pmc["SQ_INSTS_VALU"] / nr * node_rounds / kmax / ctx.world,
+                "int64_insts_share": pmc.get("SQ_INSTS_VALU_INT64", 0.0) / pmc["SQ_INSTS_VALU"],
                 "busy_frac_pmc": pmc.get("valu_busy_frac"),
-                "int64_share": pmc.get("SQ_INSTS_VALU_INT64", 0.0) / pmc["SQ_INSTS_VALU"],
-                "counters": "profiles/pmc_cfg3.json (rocprofv3 --pmc, keyed by kernel-source sha256); "
-                            "busy_frac_pmc = SQ_ACTIVE_INST_VALU x 4 / (SIMDs x dispatch cycles), which "
-                            "also counts the multi-cycle 64-bit multiplies and fp64 adds"}
+                "counters": "profiles/pmc_cfg3.json (tools/pmc_cfg3.sh: rocprofv3 --pmc over the same 10^5-instance "
+                            "batch, keyed by the kernel sources' sha256); achieved = SQ_ACTIVE_INST_VALU x 4 per "
+                            "node-round x this leg's node-rounds / this leg's HIP-event kernel time; busy_frac_pmc "
+                            "is the same busy fraction at the profiled run's own clock (GRBM_GUI_ACTIVE)"}
     return {"workload": f"cfg3: 1e5 instances x 64 nodes, complete graph, p=0.2, AVERAGE, eps=1e-6 "
                         f"(SURVEY §A.10), sharded by global instance blocks; the batch run {reps} times "
                         f"back to back (one handle each) inside the timed region",
@@ -339,7 +346,7 @@ def leg_cfg4_f32(ctx: Ctx, warm: int = 10, timed: int = 100) -> dict:
     cfg = acsim.preset("cfg4", max_rounds=warm + timed, instance_offset=ctx.rank, dtype="f32")
     with acsim.Simulator(cfg, device=ctx.dev) as sim:
         sim.round(warm)
-        sim.set_kernel_timing(True, every=10)
+        sim.set_kernel_timing(True, every=25, runs=True)
         ctx.barrier(sim)
         t0 = time.perf_counter()
         sim.round(timed)
@@ -395,7 +402,7 @@ def main():
 
     if a.warmup:
         sim.round(a.warmup)
-    sim.set_kernel_timing(not a.no_event_timing, every=a.event_every)
+    sim.set_kernel_timing(not a.no_event_timing, every=a.event_run, runs=True)
     ctx.barrier(sim)
     t0 = time.perf_counter()
     sim.round(a.steps)
@@ -442,6 +449,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": kname, "avg_launch_us": avg_launch_s * 1e6,
+                     "launch": "one round (k_bin_scatter + k_bin_gather and their boundaries), device "
+                               f"time over runs of {a.event_run} consecutive rounds",
                      "bytes_per_node_round": unit_b},
         "hbm_roofline_pct_wall": 100.0 * unit_b * value / n_gpus / 1e9 / HBM_PEAK_GBS,
         "cpu_baseline": None,

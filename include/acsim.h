@@ -212,7 +212,9 @@ int acs_get_neighbors(struct acs_sim* sim, uint32_t* out, uint64_t n);
 
 /* Kernel timing (bench measurement, §8d): while enabled, HIP events bracket the launches of the
  * round kernel on the handle's stream — every round for enable == 1, every enable-th round for
- * enable > 1 (each event pair idles the stream for a few µs, so the bench samples); 0 disables.
+ * enable > 1 (each event pair idles the stream for a few µs, so the bench samples); enable < 0
+ * brackets runs of -enable consecutive rounds with one pair each (a run ends at the end of an
+ * acs_round / acs_run call at the latest) and counts every round of a run as one launch; 0 disables.
  * acs_get_kernel_timing returns the summed device time and bracketed launch count since the
  * last reset, plus the name of the round kernel in use. */
 int acs_set_kernel_timing(struct acs_sim* sim, int enable);

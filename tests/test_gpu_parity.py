@@ -266,6 +266,28 @@ def test_kernel_timing_counts_round_launches():
         assert n == 12 and ms > 0 and (name.startswith("k_round_regular<32,5") or name.startswith("k_bin_scatter+k_bin_gather<32,5>"))
 
 
+def test_kernel_timing_runs_count_every_round():
+    """Run mode (bench.py): one event pair per run of k consecutive rounds, runs closed at the end
+    of each round(k) call, every round counted; the summed device time matches the sampled mode's
+    per-round time within a few percent and the results are untouched."""
+    cfg = preset("cfg4", n_nodes=1 << 16, max_rounds=60, termination="fixed")
+    with acsim.Simulator(cfg) as s:
+        s.set_kernel_timing(True, every=8, runs=True)
+        s.round(20)   # runs of 8, 8, 4
+        s.round(10)   # 8, 2
+        ms_r, n_r, _ = s.kernel_timing()
+        assert n_r == 30 and ms_r > 0
+        s.set_kernel_timing(True, every=1)
+        s.round(30)
+        ms_1, n_1, _ = s.kernel_timing()
+        assert n_1 == 30
+        x = s.values(0)
+    with acsim.Simulator(cfg) as s2:
+        s2.run()
+        assert np.array_equal(s2.values(0).view(np.uint64), x.view(np.uint64))
+    assert ms_r / n_r < 1.5 * ms_1 / n_1
+
+
 @pytest.mark.parametrize("name", ["cfg2_full", "dense300_clean_trim", "dense500_const_dlpsw"])
 def test_dense_two_kernel_path_still_exact(oracle_mod, name, monkeypatch):
     """The per-round dense kernels (k_dense_sort + k_dense_recv, used above 4096 nodes) on the

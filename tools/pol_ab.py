@@ -18,10 +18,15 @@ import acsim  # noqa: E402
 def main():
     preset, rounds, pols = sys.argv[1], int(sys.argv[2]), [int(v, 0) for v in sys.argv[3].split(",")]
     reps = int(sys.argv[4]) if len(sys.argv) > 4 else 2
-    cfg = acsim.preset(preset, max_rounds=rounds + 2)
+    # "<preset>_f32": the preset in fp32 mode; pol 0x10000 = the library's default policy
+    base, f32 = (preset[:-4], True) if preset.endswith("_f32") else (preset, False)
+    cfg = acsim.preset(base, max_rounds=rounds + 2, **({"dtype": "f32"} if f32 else {}))
     for rep in range(reps):
         for pol in pols:
-            os.environ["ACSIM_BIN_POL"] = str(pol)
+            if pol == 0x10000:
+                os.environ.pop("ACSIM_BIN_POL", None)
+            else:
+                os.environ["ACSIM_BIN_POL"] = str(pol)
             with acsim.Simulator(cfg) as s:
                 s.round(2)
                 s.set_kernel_timing(True, every=1)
