@@ -69,11 +69,29 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
     const uint32_t a = sel.n ? (u < sel.n ? (u / sel.bpc) * sel.bpr + sel.k0 + u % sel.bpc : 0xFFFFFFFFu) : u;
     // padding past the last source block, or a segment past its block's deliveries: idle (but
     // workgroup 0 still records a deferred finalize)
-    const bool idle = a == 0xFFFFFFFFu || (uint64_t)a * SA >= N || aoff[a] + (uint64_t)sg * chunk >= aoff[a + 1];
+    const bool noblk = a == 0xFFFFFFFFu || (uint64_t)a * SA >= N;
+    uint64_t p0 = 0, p1 = 0;
+    if (!noblk) {
+        const uint64_t s0 = aoff[a], s1 = aoff[a + 1];
+        if (pkA) {
+            // packed stream: the block's deliveries in `segs` equal parts cut at 512-position
+            // boundaries (the stream's block grid), so no segment is short and no interior cut
+            // needs the position-by-position head / tail decode
+            auto cut = [&](uint32_t k) -> uint64_t {
+                if (k == 0) return s0;
+                if (k >= segs) return s1;
+                const uint64_t c = (s0 + (s1 - s0) * k / segs + 256) & ~511ull;
+                return c < s0 ? s0 : c > s1 ? s1 : c;
+            };
+            p0 = cut(sg);
+            p1 = cut(sg + 1);
+        } else {
+            p0 = s0 + (uint64_t)sg * chunk;
+            p1 = p0 + chunk < s1 ? p0 + chunk : s1;
+        }
+    }
+    const bool idle = noblk || p0 >= p1;
     if (idle && !(fin_on && blockIdx.x == 0)) return;
-    const uint64_t pa1 = idle ? 0 : aoff[a + 1];
-    const uint64_t p0 = idle ? 0 : aoff[a] + (uint64_t)sg * chunk;
-    const uint64_t p1 = p0 + chunk < pa1 ? p0 + chunk : pa1;
     const uint64_t base = (uint64_t)a * SA;
     const uint32_t n = idle ? 0u : (uint32_t)(N - base < SA ? N - base : SA);
     {   // x block -> LDS by LDS-DMA, 16 B per lane (x is allocated with spare elements, so the
@@ -1138,9 +1156,12 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
         e = hipGetLastError();
     }
     // 14-bit packed phase-A indices (fp64 plans with source blocks of at most 2^14 senders).
-    // ACSIM_BIN_PACK: bit 0 phase A, bit 1 phase B (default 3; 0: u16 streams)
+    // ACSIM_BIN_PACK: bit 0 phase A, bit 1 phase B (default 1; 0: u16 streams).  Measured per kernel
+    // (rocprofv3, cfg4, profiles/r04_s8_pack_kernel_stats.csv): packed idxA 59.4 -> 53-54 us;
+    // packed invpos 61.7-61.8 -> 62.5-63.0 us (phase B's decode costs more than its 8 MB), so phase
+    // B keeps the u16 table by default.
     const char* pack_env = getenv("ACSIM_BIN_PACK");
-    const uint32_t pack = pack_env ? (uint32_t)strtoul(pack_env, nullptr, 10) : 3u;
+    const uint32_t pack = pack_env ? (uint32_t)strtoul(pack_env, nullptr, 10) : 1u;
     if (e == hipSuccess && !f32 && sa <= 16384) {
         if (pack & 1u) {
             const uint64_t nb = (p.Ep1 + 511) / 512;

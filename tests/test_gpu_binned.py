@@ -336,6 +336,26 @@ def _pub_variant(variant):
     return cfg, (rowptr, colidx), dict(ACSIM_BIN_SA=1024), "k_bin"
 
 
+@pytest.mark.parametrize("pack", [0, 1, 2, 3])
+def test_packed_index_streams_bit_exact(oracle_mod, pack):
+    """14-bit packed phase-A indices (bit 0) and phase-B positions (bit 1, clean d = 32 two-pass
+    plans) against the oracle: one- and two-level plans, ragged source blocks."""
+    frag = {0: None, 1: " pk14A", 2: " pk14B", 3: " pk14AB"}[pack]
+    for name, sa in (("d32_t5_eps_n50000_sa1024", None), ("two_level_d16_t5_n100000_sa256", None),
+                     ("d32_t5_dlpsw_sa2048", None)):
+        cfg, sa0 = CASES[name]
+        with env(ACSIM_BIN_SA=sa or sa0, ACSIM_BIN_PACK=pack, ACSIM_BIN_SPLIT=2 if "d32" in name else 1):
+            kb, rb, xb, tb = run_gpu(cfg)
+        if frag and "d32" in name:
+            assert frag in kb, kb
+        if pack == 0:
+            assert "pk14" not in kb, kb
+        with oracle_mod.OracleSimulator(cfg, threads=8) as o:
+            o.run()
+            assert np.array_equal(rb, o.rounds()) and np.array_equal(xb, bits(o.values(0)))
+            assert np.array_equal(tb, bits(o.spread_trace(0)))
+
+
 @pytest.mark.parametrize("variant", ["split2", "order_free", "fixup", "var"])
 def test_eps_publication_in_every_gather_variant(oracle_mod, variant):
     """Every phase-B kernel that writes a binned round's partials publishes its (min, max) for the
