@@ -279,7 +279,7 @@ def test_order_free_f32_and_wmsr(oracle_mod):
             assert np.array_equal(gx.view(np.uint8), o.values(0).view(np.uint8))
 
 
-@pytest.mark.parametrize("name,pol", [("d32_t5_eps_n50000_sa1024", p) for p in (0, 1, 2, 7, 64, 36)] +
+@pytest.mark.parametrize("name,pol", [("d32_t5_eps_n50000_sa1024", p) for p in (0, 1, 2, 7, 64, 36, 612)] +
                          [("two_level_d16_t5_n100000_sa256", p) for p in (0, 2, 128, 130, 256, 322)])
 def test_cache_policy_switches_bit_exact(oracle_mod, name, pol):
     """ACSIM_BIN_POL only changes cache policies (nontemporal runs / phase-A and phase-M stage
