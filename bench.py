@@ -152,6 +152,21 @@ def load_pmc_cfg3(kernel: str):
     return None
 
 
+def load_pmc_cfg5():
+    """cfg5's per-phase HBM traffic (profiles/pmc_cfg5.json, tools/pmc_cfg5_json.py), if it was
+    taken on these kernel sources, else None."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_cfg5.json")))
+    except Exception:
+        return None
+    if d.get("src_sha256") != src_sha256() and d.get("lib_sha256") != lib_sha256():
+        return None
+    return {"bytes_per_round": d["bytes_per_round"], "bytes_per_delivery": d["bytes_per_delivery"],
+            "phases_bytes_per_delivery": {k.split("::")[-1].split("<")[0]: v["bytes_per_delivery"]
+                                          for k, v in d["phases"].items()},
+            "source": "profiles/pmc_cfg5.json"}
+
+
 def load_pmc(kernel: str, n_nodes: int, dtype: str = "f64"):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if it was taken on this
     build of libacsim.so — same kernel name and size, and the same library sha256 or the same
@@ -335,6 +350,7 @@ def leg_cfg5(ctx: Ctx, warm: int = 2, timed: int = 8) -> dict:
                "kernel": kname, "round_kernel_ms_per_round": k_ms / max(1, k_n),
                "exchange_share": max(0.0, 1.0 - (k_ms / max(1, k_n)) / (dt / timed * 1e3)) if ctx.world > 1 else 0.0,
                "hbm_frac_unit": CFG5_BYTES_PER_NODE_ROUND * n * timed / dt / 1e9 / (HBM_PEAK_GBS * ctx.world),
+               "traffic": load_pmc_cfg5() if ctx.world == 1 else None,
                "rounds": rounds, "x_sha256": h,
                "golden_match": rounds == 10 and h == g.get("x10_sha256")}
     sim.close()
