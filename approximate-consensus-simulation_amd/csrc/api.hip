@@ -1149,10 +1149,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         if (s->binned) {
             // NP-pass phase B (slot-dependent configs: fp64, two passes only; see launch_round_binned)
             if (s->bin.split > 1 && (s->clean || (!s->f32 && s->bin.split == 2)))
-                s->kname += " split" + std::to_string(s->bin.split) +
-                            // the double-buffered kernel (t = 5, not W-MSR; otherwise the plan runs single-buffered)
-                            (s->bin.db && cfg->trim == 5 && cfg->rule != ACS_RULE_WMSR ? "db" : "") +
-                            (s->bin.pp && cfg->trim == 5 && cfg->rule != ACS_RULE_WMSR ? " pipelined" : "");
+                s->kname += " split" + std::to_string(s->bin.split);
             if (s->bin.ofree) s->kname += " orderfree";
             if (s->bin.pkA || s->bin.pkinv)   // 14-bit packed index streams
                 s->kname += std::string(" pk14") + (s->bin.pkA ? "A" : "") + (s->bin.pkinv ? "B" : "");

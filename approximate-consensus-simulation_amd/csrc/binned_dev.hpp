@@ -346,10 +346,4 @@ __device__ __forceinline__ void bin_ts(uint64_t* ts, uint64_t t0, uint64_t t1) {
 template <int D, int NP>
 constexpr uint32_t kBinPartCap = D * kBinSB / NP + D * kBinSB / 16;   // + 1/16 of the image: run-length variation and padding
 
-// Double-buffered NP-pass phase B (ACSIM_BIN_DB): two buffers of kBinPartCapDB<D, NP> elements; part
-// k + 1's DMA goes to the other buffer while part k is picked up.  NP = 4 at d = 32 needs the LDS of
-// the single-buffered NP = 2 kernel (2 x 2304 fp64 = 36 KiB: 4 workgroups per CU).
-template <int D, int NP>
-constexpr uint32_t kBinPartCapDB = D * kBinSB / NP + D * kBinSB / 32;
-
 }  // namespace acs

@@ -179,9 +179,6 @@ struct BinnedPlan {
     bool ofree = false;                 // order-free phase B (rid, no invpos)
     bool var = false;                   // CSR rows below the compiled degree (kEllNone columns)
     uint32_t split = 1;                 // phase-B passes over the image (ACSIM_BIN_SPLIT; 1 = whole image)
-    uint32_t db = 0;                    // 1: the passes double-buffered (ACSIM_BIN_DB; clean fp64 d = 32)
-    uint32_t pp = 0;                    // persistent pipelined phase B: its workgroups (ACSIM_BIN_PP; 0 = off)
-    uint32_t pplate = 0;                // ... with the next block's positions loaded after the rule (ACSIM_BIN_PP=2)
     uint32_t pol = 0;                   // cache-policy switches (round_binned.hip kPol*)
     uint32_t rstride = 0;               // bytes per receiver block in rid
     uint8_t* rid = nullptr;             // [Q][rstride] receiver inside block b of each image position (ofree)

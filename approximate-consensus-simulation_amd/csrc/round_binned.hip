@@ -261,21 +261,18 @@ __global__ __launch_bounds__(256) void k_bin_fixup(const uint4* __restrict__ fix
 // PK14 (clean d = 32 plans): `invpos` points at the 14-bit packed positions
 // (binned_dev.hpp pk14inv layout) instead of the u16 table.
 template <int D, int T, bool WMSR = false, bool FAULTY = false, typename VT = double, int NP = 1, bool VAR = false,
-          bool FIX = false, bool PK14 = false, bool DB = false>
-__global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) : (FIX && NP > 1 && (T || WMSR)) ? 4 : 1) void k_bin_gather(const RoundArgs a, const VT* __restrict__ stage,
+          bool FIX = false, bool PK14 = false>
+__global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) : FIX && NP > 1 && (T || WMSR) ? 4 : 1) void k_bin_gather(const RoundArgs a, const VT* __restrict__ stage,
                                                        const uint16_t* __restrict__ invpos,
                                                        const uint2* __restrict__ tiles, uint32_t nrun, uint32_t Q,
                                                        uint32_t Qc, uint32_t pol) {
     static_assert(D % 8 == 0, "invpos is read 8 slots at a time");
     static_assert(!PK14 || (D == 32 && !FAULTY && !FIX && !VAR), "packed positions: clean d = 32 plans");
     static_assert(!(FIX && FAULTY), "FIX replaces the tagged resolution");
-    static_assert(!DB || (NP > 1 && !FAULTY && !FIX && !VAR && !PK14 && sizeof(VT) == 8),
-                  "double-buffered parts: clean fp64 NP-pass plans");
     constexpr bool FLT = FAULTY || FIX;   // a fault schedule or loss: receiver status and drop mask
     // runs are padded to 16-byte multiples; nrun <= D*kBinSB/16 (checked when the plan is built)
     __shared__ __attribute__((aligned(16)))
-    VT raw[DB ? kBinPartCapDB<D, NP> : NP > 1 ? kBinPartCap<D, NP> : D * kBinSB + D * kBinSB / 16 * (16 / sizeof(VT) - 1)];
-    __shared__ __attribute__((aligned(16))) VT raw2[DB ? kBinPartCapDB<D, NP> : 2];   // DB: odd parts' buffer
+    VT raw[NP > 1 ? kBinPartCap<D, NP> : D * kBinSB + D * kBinSB / 16 * (16 / sizeof(VT) - 1)];
     InstState* S = a.st;
     if (S->done) return;
     const uint64_t t0 = a.ts ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -300,7 +297,7 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
     // NP-pass blocks of at most 64 runs: every wave fetches all descriptors first (one per lane)
     // and issues part 0's DMA before anything else is in flight, so the only wait ahead of the
     // first transfer is the descriptor load itself; later parts issue from registers.
-    const bool pf = NP > 1 && (DB || (nrun <= 64 && !(pol & kPolNoPf)));   // DB plans hold <= 64 runs
+    const bool pf = NP > 1 && nrun <= 64 && !(pol & kPolNoPf);
     uint2 pdsc = make_uint2(0u, 0u);
     uint32_t pnxt = 0;
     if (pf) {
@@ -408,62 +405,6 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
         if (a.ts) t1 = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
         for (int t = 0; t < D; ++t) v[1 + t] = raw[pos_of(t)];
-    } else if constexpr (DB) {
-        // Double-buffered parts: one barrier per part.  After it, part k has landed in every wave
-        // (the barrier's vmcnt(0) covers the only DMA in flight, part k's own) and every wave is past
-        // part k - 1's pick-up, so part k + 1's DMA can go to that buffer before part k is picked up.
-        // (v starts defined: with undefined values the selects of part 0 became branches.)
-#pragma unroll
-        for (int t = 0; t < D; ++t) v[1 + t] = VT(0);
-#pragma unroll
-        for (uint32_t k = 0; k < (uint32_t)NP; ++k) {
-            const uint32_t j0 = k * nrun / NP, j1 = (k + 1) * nrun / NP;
-            uint32_t lo = __builtin_amdgcn_readlane(pdsc.y, j0);
-            uint32_t hi = j1 < nrun ? __builtin_amdgcn_readlane(pdsc.y, j1) : __builtin_amdgcn_readlane(pnxt, nrun - 1);
-            __syncthreads();
-            // lo / hi defined here for the compiler: otherwise it hoisted every part's 32 pick-up
-            // addresses to the kernel's start (128 live VGPRs, hundreds of bytes of spills)
-            asm volatile("" : "+s"(lo), "+s"(hi));
-            const uint32_t len = hi - lo;   // slot in this part <=> (pos - lo) < len, unsigned
-            if (k == 0 && a.ts) t1 = __builtin_amdgcn_s_memrealtime();
-            if (k + 1 < (uint32_t)NP) {
-                const uint32_t j2 = (k + 2) * nrun / NP;
-                bin_dma_runs_pf(pdsc, pnxt, j1 + w * (j2 - j1) / NW, j1 + (w + 1) * (j2 - j1) / NW, stage,
-                                (k & 1) ? raw : raw2, hi);
-            }
-            // LDS byte offset of this part's buffer
-            const uint32_t bo = (uint32_t)reinterpret_cast<uintptr_t>(
-                (__attribute__((address_space(3))) const VT*)((k & 1) ? raw2 : raw));
-#pragma unroll
-            for (int q = 0; q < D / 8; ++q) {
-                // every lane reads all 8 slots (offset 0 when out of this part), then selects.  The
-                // reads are asm so that the compiler cannot turn them into exec-masked branches (it
-                // did: one lgkmcnt(0) per read, and spills); their wait is the asm below.
-                double tv[8];
-                uint32_t off[8];   // offset in this part (wraps above len below lo)
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    off[e] = pos_of(8 * q + e) - lo;
-                    const uint32_t ad = bo + (off[e] < len ? off[e] : 0u) * 8u;
-                    asm volatile("ds_read_b64 %0, %1" : "=v"(tv[e]) : "v"(ad) : "memory");
-                }
-                // the offsets pass through the wait too, so the selects recompute their compares
-                // (kept live across it, the 64-bit masks had filled the SGPRs and spilled)
-                asm volatile("s_waitcnt lgkmcnt(0)"
-                             : "+v"(tv[0]), "+v"(tv[1]), "+v"(tv[2]), "+v"(tv[3]), "+v"(tv[4]), "+v"(tv[5]),
-                               "+v"(tv[6]), "+v"(tv[7]), "+v"(off[0]), "+v"(off[1]), "+v"(off[2]), "+v"(off[3]),
-                               "+v"(off[4]), "+v"(off[5]), "+v"(off[6]), "+v"(off[7])
-                             :
-                             : "memory");
-#pragma unroll
-                for (int e = 0; e < 8; ++e) v[1 + 8 * q + e] = off[e] < len ? tv[e] : v[1 + 8 * q + e];
-                // the selects happen here: left free, the compiler sank every part's selects to the
-                // sort and kept all parts' values live (399 VGPRs)
-                asm volatile(""
-                             : "+v"(v[1 + 8 * q]), "+v"(v[2 + 8 * q]), "+v"(v[3 + 8 * q]), "+v"(v[4 + 8 * q]),
-                               "+v"(v[5 + 8 * q]), "+v"(v[6 + 8 * q]), "+v"(v[7 + 8 * q]), "+v"(v[8 + 8 * q]));
-            }
-        }
     } else {
 #pragma unroll
         // Unrolled: the first part skips the p >= lo test and the last part the p < hi test.  This
@@ -610,202 +551,6 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
     }
     block_minmax_store<kBinSB>(mn, mx, a.partial + b, a.eacc);
     if (a.ts) bin_ts(a.ts, t0, t1);
-}
-
-// ------------------------------------------------------------------------------ phase B, pipelined
-// Persistent two-pass phase B (ACSIM_BIN_PP=1; clean fp64 d = 32 plans of <= 64 runs, DESIGN.md
-// §5.10).  The same blocks, parts, pick-up and rule as k_bin_gather<D, T, WMSR, false, double, 2>, but
-// each workgroup walks the virtual block ids blockIdx.x, + gridDim.x, ... (gridDim.x a multiple of 8,
-// so every block of a workgroup maps to the same XCD as in k_bin_gather) and issues block n+1's
-// part-0 DMA, invpos and x_i loads before block n's sort, rule and x store: the DMA of one block no
-// longer waits for the previous block's compute tail.  Block n's (min, max) is folded by thread 0
-// after the next block's first barrier (no extra barrier).
-// An empty asm that takes 8 values in and out: the code producing them cannot sink below it.
-__device__ __forceinline__ void pin8(double* x) {
-    asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]));
-}
-
-// LATE: the next block's positions are loaded after this block's rule too (fewer live VGPRs during
-// the sort; their latency is then exposed at the next block's first barrier).
-template <int D, int T, bool WMSR = false, bool LATE = false>
-__global__ __launch_bounds__(kBinSB) void k_bin_gather_pp(const RoundArgs a, const double* __restrict__ stage,
-                                                          const uint16_t* __restrict__ invpos,
-                                                          const uint2* __restrict__ tiles, uint32_t nrun, uint32_t Q,
-                                                          uint32_t Qc) {
-    using VT = double;
-    constexpr int NP = 2;
-    constexpr uint32_t NW = kBinSB / 64;
-    static_assert(D % 8 == 0, "invpos is read 8 slots at a time");
-    __shared__ __attribute__((aligned(16))) VT raw[kBinPartCap<D, NP>];
-    __shared__ double2 red[NW];
-    InstState* S = a.st;
-    if (S->done) return;
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t nv = 8 * Qc;
-    const uint32_t qend = a.qhi < Q ? a.qhi : Q;
-    auto blk = [&](uint32_t v) { return a.qlo + (v & 7u) * Qc + (v >> 3); };
-    // partial slots past this partition's blocks: neutral (the finalize folds a.nblk)
-    if (threadIdx.x == 0)
-        for (uint32_t v = blockIdx.x; v < nv; v += gridDim.x) {
-            const uint32_t b = blk(v);
-            if (b >= Q && b < a.qhi && b < a.nblk) a.partial[b] = make_double2(kInf, -kInf);
-        }
-    auto next_real = [&](uint32_t v) {   // first virtual id >= v (same residue) of a real block; nv if none
-        while (v < nv && blk(v) >= qend) v += gridDim.x;
-        return v;
-    };
-    uint32_t v = next_real(blockIdx.x);
-    if (v >= nv) return;
-    const uint32_t j1 = nrun / NP;
-    // block state: descriptors (one per lane), x_i, positions
-    uint2 pdsc = make_uint2(0u, 0u);
-    uint32_t pnxt = 0;
-    uint32_t b = blk(v);
-    {
-        const uint2* tb = tiles + (uint64_t)b * (nrun + 1);
-        if (lane < nrun) {
-            pdsc = tb[lane];
-            pnxt = tb[lane + 1].y;
-        }
-    }
-    bin_dma_runs_pf(pdsc, pnxt, w * j1 / NW, (w + 1) * j1 / NW, stage, raw, 0u);
-    using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
-    uint4 ip[D / 8];
-    auto load_xi = [&](uint32_t bb) {
-        const uint64_t li = (uint64_t)bb * kBinSB + threadIdx.x;
-        return li < a.nrows ? reinterpret_cast<const VT*>(a.xin)[a.row0 + li] : VT(0);
-    };
-    auto load_ip = [&](uint32_t bb) {
-        const u32x4* ipn = reinterpret_cast<const u32x4*>(invpos) + (uint64_t)bb * (D / 8) * kBinSB + threadIdx.x;
-#pragma unroll
-        for (int q = 0; q < D / 8; ++q) {
-            const u32x4 t4 = __builtin_nontemporal_load(ipn + q * kBinSB);
-            ip[q] = make_uint4(t4.x, t4.y, t4.z, t4.w);
-        }
-    };
-    VT xi = load_xi(b);
-    load_ip(b);
-    auto pos_of = [&](int t) -> uint32_t {
-        const uint4& u = ip[t / 8];
-        const uint32_t wd = (t & 6) == 0 ? u.x : (t & 6) == 2 ? u.y : (t & 6) == 4 ? u.z : u.w;
-        return (t & 1) ? wd >> 16 : wd & 0xFFFFu;
-    };
-    bool have_prev = false;
-    uint32_t vprev = 0, bprev = 0;
-    VT v_[D + 1];
-    const uint32_t bo = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const VT*)raw);
-    // pick-up of the slots whose image position p lies in [lo, lo + len) (unsigned (p - lo) < len):
-    // every lane reads all 8 slots of a group (offset 0 when out of the part), then selects.  The reads
-    // are asm and their wait is the asm after them, with the offsets passed through it: written in C,
-    // the compiler made the reads exec-masked branches with one wait each, and sank the selects
-    // (keeping both parts' values live).
-    auto pick = [&](uint32_t lo, uint32_t len) {
-        // the packed positions pass through an asm per part, so the 32 unpacked ones are not kept
-        // live from part 0 to part 1 (16 VGPRs more)
-#pragma unroll
-        for (int q = 0; q < D / 8; ++q) asm volatile("" : "+v"(ip[q].x), "+v"(ip[q].y), "+v"(ip[q].z), "+v"(ip[q].w));
-#pragma unroll
-        for (int q = 0; q < D / 8; ++q) {
-            double tv[8];
-            uint32_t off[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                off[e] = pos_of(8 * q + e) - lo;
-                const uint32_t ad = bo + (off[e] < len ? off[e] : 0u) * 8u;
-                asm volatile("ds_read_b64 %0, %1" : "=v"(tv[e]) : "v"(ad) : "memory");
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)"
-                         : "+v"(tv[0]), "+v"(tv[1]), "+v"(tv[2]), "+v"(tv[3]), "+v"(tv[4]), "+v"(tv[5]), "+v"(tv[6]),
-                           "+v"(tv[7]), "+v"(off[0]), "+v"(off[1]), "+v"(off[2]), "+v"(off[3]), "+v"(off[4]),
-                           "+v"(off[5]), "+v"(off[6]), "+v"(off[7])
-                         :
-                         : "memory");
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v_[1 + 8 * q + e] = off[e] < len ? tv[e] : v_[1 + 8 * q + e];
-            pin8(v_ + 1 + 8 * q);
-        }
-    };
-    while (true) {
-        const uint32_t hi0 = __builtin_amdgcn_readlane(pdsc.y, j1);   // part 0 = image [0, hi0)
-        __syncthreads();   // B1: part 0 landed; red[] of the previous block written
-        if (have_prev && threadIdx.x == 0) {
-            double mn = red[0].x, mx = red[0].y;
-#pragma unroll
-            for (int k = 1; k < (int)NW; ++k) {
-                mn = __builtin_fmin(mn, red[k].x);
-                mx = __builtin_fmax(mx, red[k].y);
-            }
-            a.partial[bprev] = make_double2(mn, mx);
-            if (a.eacc) {
-                unsigned long long* pe = a.eacc + (vprev % kEaccSlots) * kEaccStride;
-                __hip_atomic_fetch_max(pe, ~ord_of(mn), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_fetch_max(pe + 1, ord_of(mx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-#pragma unroll
-        for (int t = 0; t <= D; ++t) v_[t] = VT(0);   // no values carried across blocks (nor registers)
-        pick(0u, hi0);   // part 0: image [0, hi0)
-        const uint32_t lo1 = hi0;
-        __syncthreads();   // B2: every wave is past part 0's pick-up
-        bin_dma_runs_pf(pdsc, pnxt, j1 + w * (nrun - j1) / NW, j1 + (w + 1) * (nrun - j1) / NW, stage, raw, lo1);
-        const uint32_t vn = next_real(v + gridDim.x);
-        const uint32_t bn = vn < nv ? blk(vn) : 0u;
-        uint2 ndsc = make_uint2(0u, 0u);
-        uint32_t nnxt = 0;
-        if (vn < nv && lane < nrun) {
-            const uint2* tb = tiles + (uint64_t)bn * (nrun + 1);
-            ndsc = tb[lane];
-            nnxt = tb[lane + 1].y;
-        }
-        __syncthreads();   // B3: part 1 landed (and the next block's descriptors)
-        pick(lo1, 0u - lo1);   // part 1 (the last): image [lo1, end): (p - lo1) < 2^32 - lo1
-        __syncthreads();   // B4: every wave is past part 1's pick-up: the buffer and ip are free
-        const uint64_t li = (uint64_t)b * kBinSB + threadIdx.x;
-        const bool live = li < a.nrows;
-        if (vn < nv) {   // the next block's part 0 and positions, in flight during this block's rule
-            pdsc = ndsc;
-            pnxt = nnxt;
-            bin_dma_runs_pf(pdsc, pnxt, w * j1 / NW, (w + 1) * j1 / NW, stage, raw, 0u);
-            if constexpr (!LATE) load_ip(bn);
-        }
-        double mn = kInf, mx = -kInf;
-        if (live) {
-            v_[0] = xi;
-            const VT res = apply_rule_reg<D, T, WMSR>(a.rule, v_);
-            reinterpret_cast<VT*>(a.xout)[a.row0 + li] = res;
-            mn = res;
-            mx = res;
-        }
-        if (vn < nv) {   // after the rule: fewer live VGPRs while it sorts
-            xi = load_xi(bn);
-            if constexpr (LATE) load_ip(bn);
-        }
-        mn = wave_min(mn);
-        mx = wave_max(mx);
-        if (lane == 0) red[w] = make_double2(mn, mx);
-        have_prev = true;
-        vprev = v;
-        bprev = b;
-        if (vn >= nv) break;
-        v = vn;
-        b = bn;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double mn = red[0].x, mx = red[0].y;
-#pragma unroll
-        for (int k = 1; k < (int)NW; ++k) {
-            mn = __builtin_fmin(mn, red[k].x);
-            mx = __builtin_fmax(mx, red[k].y);
-        }
-        a.partial[bprev] = make_double2(mn, mx);
-        if (a.eacc) {
-            unsigned long long* pe = a.eacc + (vprev % kEaccSlots) * kEaccStride;
-            __hip_atomic_fetch_max(pe, ~ord_of(mn), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_max(pe + 1, ord_of(mx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
 }
 
 // ------------------------------------------------------------------------------ phase B, order-free
@@ -1544,58 +1289,24 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     if (e == hipSuccess && !ofree) {
         const char* v = getenv("ACSIM_BIN_SPLIT");
         uint32_t np = v ? (uint32_t)strtoul(v, nullptr, 10) : (!f32 && G.D == 32 ? 2u : 1u);
-        // double-buffered passes (ACSIM_BIN_DB=1; clean fp64 d = 32, <= 64 runs): 4 passes by default,
-        // ACSIM_BIN_SPLIT=8 for 8; plans whose parts overflow a buffer fall back to 2 passes.  Only the
-        // t = 5 non-W-MSR rules have the DB kernel; the others run the single-buffered 4-pass kernel on
-        // the same plan (its parts are unions of DB parts and its buffer holds kBinPartCap<32, 4> >=
-        // 2 kBinPartCapDB<32, 8> and >= kBinPartCapDB<32, 4>)
-        const char* vdb = getenv("ACSIM_BIN_DB");
-        bool db = vdb && strtoul(vdb, nullptr, 10) == 1 && clean && !tagged && !f32 && !var && G.D == 32 &&
-                  p.nrun <= 64;
-        if (db) np = np == 8 ? 8u : 4u;
-        if (np < 1 || (np > 4 && !db) || var) np = 1;   // CSR plans: single pass (the VAR kernels)
+        if (np < 1 || np > 4 || var) np = 1;   // CSR plans: single pass (the VAR kernels)
         if (f32 && tagged && np > 1) np = 1;   // tagged fp32 phase B: one pass (no split instantiation)
         if (tagged && np > 2) np = 2;          // tagged fp64 phase B: two passes at most
         if (np > 1) {
             const uint32_t D = G.D;
+            const uint32_t cap = D * kBinSB / np + D * kBinSB / 16;   // kBinPartCap<D, np>
             std::vector<uint2> h(((uint64_t)p.nrun + 1) * G.Q);
             e = hipMemcpy(h.data(), p.tiles, h.size() * sizeof(uint2), hipMemcpyDeviceToHost);
-            for (int attempt = 0; attempt < 2; ++attempt) {
-                // kBinPartCapDB<D, np> / kBinPartCap<D, np>
-                const uint32_t cap = db ? D * kBinSB / np + D * kBinSB / 32 : D * kBinSB / np + D * kBinSB / 16;
-                bool fits = e == hipSuccess && p.nrun >= np;
-                for (uint32_t b = 0; fits && b < G.Q; ++b) {
-                    const uint2* row = h.data() + (uint64_t)b * (p.nrun + 1);
-                    // the NP-pass kernel's skipped bound tests: part 0 starts at image offset 0, and the
-                    // image is non-empty (padding lanes read invpos 0, which must lie in the last part)
-                    fits = row[0].y == 0 && row[p.nrun].y > 0;
-                    for (uint32_t k = 0; fits && k < np; ++k)
-                        fits = row[(k + 1) * p.nrun / np].y - row[k * p.nrun / np].y <= cap;
-                }
-                if (fits) {
-                    p.split = np;
-                    p.db = db ? 1u : 0u;
-                    break;
-                }
-                if (!db) break;
-                db = false;   // one retry: the single-buffered two-pass kernel
-                np = 2;
+            bool fits = e == hipSuccess && p.nrun >= np;
+            for (uint32_t b = 0; fits && b < G.Q; ++b) {
+                const uint2* row = h.data() + (uint64_t)b * (p.nrun + 1);
+                // the NP-pass kernel's skipped bound tests: part 0 starts at image offset 0, and the
+                // image is non-empty (padding lanes read invpos 0, which must lie in the last part)
+                fits = row[0].y == 0 && row[p.nrun].y > 0;
+                for (uint32_t k = 0; fits && k < np; ++k)
+                    fits = row[(k + 1) * p.nrun / np].y - row[k * p.nrun / np].y <= cap;
             }
-            // persistent pipelined phase B (ACSIM_BIN_PP=1; clean fp64 d = 32 two-pass plans of <= 64
-            // runs): 4 workgroups per CU (the LDS bound), a multiple of 8 (ACSIM_BIN_PPG overrides)
-            const char* vpp = getenv("ACSIM_BIN_PP");
-            const uint32_t ppm = vpp ? (uint32_t)strtoul(vpp, nullptr, 10) : 0u;   // 2: LATE positions
-            p.pplate = ppm == 2 ? 1u : 0u;
-            if (e == hipSuccess && (ppm == 1 || ppm == 2) && p.split == 2 && !p.db && clean &&
-                !tagged && !f32 && !var && D == 32 && p.nrun <= 64 && !(pack & 2u)) {
-                int dev = 0, ncu = 0;
-                e = hipGetDevice(&dev);
-                if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-                uint32_t g = (uint32_t)ncu * 4u;
-                if (const char* vg = getenv("ACSIM_BIN_PPG")) g = (uint32_t)strtoul(vg, nullptr, 10);
-                g = g / 8 * 8;
-                if (e == hipSuccess && g >= 8) p.pp = g;
-            }
+            if (fits) p.split = np;
             // 14-bit packed positions for phase B: clean fp64 d = 32 two-pass
             // plans whose every block image holds fewer than 2^14 entries
             uint32_t mxpos = 0;
@@ -1684,16 +1395,7 @@ static hipError_t binned_set_lds_attributes() {
 // clean phase B in p.split (2..4) passes
 #define ACS_BIN_NP_LAUNCH(DD, TT, W, VT_, SRC)                                                         \
     {                                                                                                  \
-        if (p.db && DD == 32 && TT == 5 && !W && sizeof(VT_) == 8) {                                   \
-            if constexpr (DD == 32 && TT == 5 && !W && sizeof(VT_) == 8) {                             \
-                if (p.split == 8)                                                                      \
-                    hipLaunchKernelGGL((k_bin_gather<DD, TT, W, false, VT_, 8, false, false, false, true>), \
-                                       grid, dim3(kBinSB), 0, s, a, SRC, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol); \
-                else                                                                                   \
-                    hipLaunchKernelGGL((k_bin_gather<DD, TT, W, false, VT_, 4, false, false, false, true>), \
-                                       grid, dim3(kBinSB), 0, s, a, SRC, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol); \
-            }                                                                                          \
-        } else if (p.split == 2 && p.pkinv) {                                                          \
+        if (p.split == 2 && p.pkinv) {                                                                 \
             if constexpr (DD == 32 && sizeof(VT_) == 8)                                                    \
                 hipLaunchKernelGGL((k_bin_gather<DD, TT, W, false, VT_, 2, false, false, true>), grid,     \
                                    dim3(kBinSB), 0, s, a, SRC, reinterpret_cast<const uint16_t*>(p.pkinv), \
@@ -1856,17 +1558,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
         else if (clean && p.ofree)                                                                       \
             hipLaunchKernelGGL((k_bin_gather_of<DD, TT>), grid, dim3(kBinSB), 0, s, a, last, p.rid,         \
                                p.rstride, p.tiles, p.nrun, p.Q, Qc);                                     \
-        else if (clean && p.pp && DD == 32 && TT == 5 && !w_) {                                         \
-            if constexpr (DD == 32 && TT == 5) {                                                         \
-                const uint32_t g_ = p.pp < 8 * Qc ? p.pp : 8 * Qc;                                       \
-                if (p.pplate)                                                                            \
-                    hipLaunchKernelGGL((k_bin_gather_pp<DD, TT, false, true>), dim3(g_), dim3(kBinSB), 0, s, \
-                                       a, last, p.invpos, p.tiles, p.nrun, p.Q, Qc);                      \
-                else                                                                                     \
-                    hipLaunchKernelGGL((k_bin_gather_pp<DD, TT>), dim3(g_), dim3(kBinSB), 0, s, a, last, \
-                                       p.invpos, p.tiles, p.nrun, p.Q, Qc);                               \
-            }                                                                                            \
-        } else if (clean && p.split > 1 && w_)                                                           \
+        else if (clean && p.split > 1 && w_)                                                             \
             ACS_BIN_NP_LAUNCH(DD, TT, true, double, last)                                                \
         else if (clean && p.split > 1)                                                                   \
             ACS_BIN_NP_LAUNCH(DD, TT, false, double, last)                                               \

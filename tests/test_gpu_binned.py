@@ -437,90 +437,6 @@ def test_split_more_passes_match_oracle(oracle_mod, np_):
         assert np.array_equal(tb, bits(o.spread_trace(0)))
 
 
-@pytest.mark.parametrize("np_", [4, 8])
-@pytest.mark.parametrize("name", ["d32_t5_eps_n50000_sa1024", "d32_t5_dlpsw_sa2048", "cfg4_shape_2e17",
-                                  "d32_t5_midpoint", "d32_t5_wmsr", "d32_t0_midpoint", "d32_t5_split_pub"])
-def test_double_buffered_phase_b_matches_oracle(oracle_mod, name, np_):
-    """Double-buffered NP-pass phase B (ACSIM_BIN_DB=1: part k + 1's DMA in flight while part k is
-    picked up) against the oracle, bit for bit, across round(k) calls that end
-    mid-chunk.  t != 5 and W-MSR plans keep the same parts on the single-buffered kernel."""
-    extra = dict(topology="regular", degree=32, eps=1e-9, max_rounds=120, seed=77, trace_spread=True)
-    if name == "d32_t5_midpoint":
-        cfg, sa = Config(n_nodes=33333, rule="midpoint", trim=5, **extra), 1024
-    elif name == "d32_t5_wmsr":
-        cfg, sa = Config(n_nodes=33333, rule="wmsr", trim=5, **extra), 1024
-    elif name == "d32_t0_midpoint":
-        cfg, sa = Config(n_nodes=33333, rule="midpoint", trim=0, **extra), 2048
-    elif name == "d32_t5_split_pub":   # EPS verdict publication (ACSIM_EPS_PUB) through the DB kernel
-        cfg, sa = Config(n_nodes=40000, rule="trimmed", trim=5, **dict(extra, max_rounds=60, seed=31)), 2048
-    else:
-        cfg, sa = CASES[name]
-    db_kernel = name not in ("d32_t5_wmsr", "d32_t0_midpoint")
-    with env(ACSIM_BIN_SA=sa, ACSIM_BIN_SPLIT=np_, ACSIM_BIN_DB=1):
-        with acsim.Simulator(cfg, device=0) as g:
-            kb = g.kernel_name()
-            g.round(3)
-            g.round(17)
-            g.run()
-            rb, xb, tb = g.rounds(), bits(g.values(0)), bits(g.spread_trace(0))
-    # 8 parts of a graph with few source blocks (2-3 runs per part) may overflow a part buffer: the
-    # plan then falls back to the single-buffered two-pass kernel (binned_build)
-    if not (np_ == 8 and " split2" in kb):
-        assert (f" split{np_}db" in kb) == db_kernel and f" split{np_}" in kb, kb
-    with oracle_mod.OracleSimulator(cfg, threads=8) as o:
-        o.run()
-        assert np.array_equal(rb, o.rounds()) and np.array_equal(xb, bits(o.values(0)))
-        assert np.array_equal(tb, bits(o.spread_trace(0)))
-
-
-@pytest.mark.parametrize("mode", [1, 2])
-@pytest.mark.parametrize("name", ["d32_t5_eps_n50000_sa1024", "d32_t5_dlpsw_sa2048", "cfg4_shape_2e17",
-                                  "d32_t5_midpoint", "d32_t5_wmsr", "d32_t5_few_workgroups",
-                                  "d32_t5_chunked_partitions"])
-def test_pipelined_phase_b_matches_oracle(oracle_mod, name, mode):
-    """Persistent pipelined phase B (ACSIM_BIN_PP=1, =2 with the positions loaded after the rule;
-    DESIGN.md §5.10): each workgroup walks several receiver blocks and issues the next block's part-0
-    DMA before this block's rule.  Against the oracle bit for bit across round(k) calls that end
-    mid-chunk (EPS verdict publication included), with few workgroups (many blocks each), and over
-    2 chunked virtual partitions (receiver-block sub-ranges per launch).  W-MSR plans keep the
-    two-pass kernel."""
-    extra = dict(topology="regular", degree=32, eps=1e-9, max_rounds=120, seed=77, trace_spread=True)
-    envs = dict(ACSIM_BIN_PP=mode)
-    parts = 0
-    if name == "d32_t5_midpoint":
-        cfg, sa = Config(n_nodes=33333, rule="midpoint", trim=5, **extra), 1024
-    elif name == "d32_t5_wmsr":
-        cfg, sa = Config(n_nodes=33333, rule="wmsr", trim=5, **extra), 1024
-    elif name == "d32_t5_few_workgroups":
-        cfg, sa = Config(n_nodes=70001, rule="trimmed", trim=5, **extra), 2048
-        envs["ACSIM_BIN_PPG"] = 16
-    elif name == "d32_t5_chunked_partitions":
-        # 2 partitions of 2^16 rows in 4 chunks of 64 receiver blocks (chunks need whole source
-        # blocks: rows_per % (4 * SA) == 0), 16 workgroups per launch: 4 blocks each
-        cfg, sa = Config(n_nodes=1 << 17, rule="trimmed", trim=5, **extra), 4096
-        envs.update(ACSIM_XCHUNKS=4, ACSIM_BIN_PPG=16)
-        parts = 2
-    else:
-        cfg, sa = CASES[name]
-    with env(ACSIM_BIN_SA=sa, **envs):
-        with (acsim.Simulator(cfg, partitions=parts) if parts else acsim.Simulator(cfg, device=0)) as g:
-            kb = g.kernel_name()
-            g.round(3)
-            g.round(17)
-            g.run()
-            rb, xb, tb = g.rounds(), bits(g.values(0)), bits(g.spread_trace(0))
-            if parts:
-                for q in range(parts):
-                    assert np.array_equal(bits(g.partition_values(q)), xb), f"copy {q} differs"
-    assert (" pipelined" in kb) == (name != "d32_t5_wmsr"), kb
-    if parts:
-        assert "xchunks4" in kb, kb
-    with oracle_mod.OracleSimulator(cfg, threads=8) as o:
-        o.run()
-        assert np.array_equal(rb, o.rounds()) and np.array_equal(xb, bits(o.values(0)))
-        assert np.array_equal(tb, bits(o.spread_trace(0)))
-
-
 @pytest.mark.parametrize("name", ["faulty_d32_t5_byzrandom_drop_sa1024", "faulty_d32_dlpsw_split_sa2048",
                                   "faulty_cfg4_byz_shape_2e17"])
 def test_split_faulty_matches_oracle(oracle_mod, name):

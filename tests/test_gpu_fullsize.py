@@ -61,43 +61,6 @@ def test_cfg4_full_size_bit_exact(oracle_mod, name, over):
     assert np.array_equal(bits(gt), bits(ot)), "spread traces differ"
 
 
-@pytest.mark.parametrize("np_", [4, 8])
-def test_cfg4_double_buffered_phase_b_matches_golden(np_):
-    """The double-buffered NP-pass phase B (ACSIM_BIN_DB=1) on the bench workload:
-    100 FIXED rounds against the committed golden hash, bit for bit."""
-    old = {k: os.environ.get(k) for k in ("ACSIM_BIN_DB", "ACSIM_BIN_SPLIT")}
-    os.environ.update(ACSIM_BIN_DB="1", ACSIM_BIN_SPLIT=str(np_))
-    try:
-        kname, gr, gx, gt = run_gpu(preset("cfg4", max_rounds=100, trace_spread=True))
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-    assert f" split{np_}db" in kname, kname
-    assert int(gr[0]) == 100
-    assert sha256_values(gx) == GOLDEN["cfg4"]["fixed100_x_sha256"]
-
-
-@pytest.mark.parametrize("mode", [1, 2])
-def test_cfg4_pipelined_phase_b_matches_golden(mode):
-    """The persistent pipelined phase B (ACSIM_BIN_PP) on the bench workload: 100
-    FIXED rounds against the committed golden hash, bit for bit."""
-    old = os.environ.get("ACSIM_BIN_PP")
-    os.environ["ACSIM_BIN_PP"] = str(mode)
-    try:
-        kname, gr, gx, gt = run_gpu(preset("cfg4", max_rounds=100, trace_spread=True))
-    finally:
-        if old is None:
-            os.environ.pop("ACSIM_BIN_PP", None)
-        else:
-            os.environ["ACSIM_BIN_PP"] = old
-    assert " pipelined" in kname, kname
-    assert int(gr[0]) == 100
-    assert sha256_values(gx) == GOLDEN["cfg4"]["fixed100_x_sha256"]
-
-
 def test_cfg4_f32_fixed100_matches_golden():
     """fp32 mode of the bench workload (100 FIXED rounds) against the oracle-written hash that
     bench.py's cfg4_f32 leg checks."""
