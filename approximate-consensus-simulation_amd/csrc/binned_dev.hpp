@@ -23,6 +23,7 @@ constexpr uint32_t kPolSc1Store = 64;   // phase A: write-through (sc1) stage st
 constexpr uint32_t kPolNtStoreM = 128;  // phase M (two-level plans): nontemporal stage-2 stores
 constexpr uint32_t kPolSc1StoreM = 256; // phase M: write-through (sc1) stage-2 stores
 constexpr uint32_t kPolSc1X = 512;      // phase B: write-through (sc1) stores of x^{r+1}
+constexpr uint32_t kPolClampPick = 1024; // phase B (NP = 2): pick-up by clamped index into a zero slot, OR-merged
 // Default switches (the stage-store bits are chosen per plan).  Until round 4 the
 // stream's store flavour was a runtime argument, and the compiler merged the nontemporal and the
 // plain store of its two branches into one plain store: every "nontemporal stage store" measured
@@ -34,7 +35,8 @@ constexpr uint32_t kPolSc1X = 512;      // phase B: write-through (sc1) stores o
 // 7.60 against 7.86 ms per round for plain ones (the 16 GiB of stages far exceed the MALL)
 constexpr uint32_t kPolOneLevelStores = kPolSc1Store;
 constexpr uint32_t kPolTwoLevelStores = kPolNtStore | kPolNtStoreM;
-constexpr uint32_t kPolDefault = kPolNtInv | kPolBfPick;   // measured (cfg4): phase B 80 -> 71 (nt invpos) -> 63.2 us (pick-up)
+constexpr uint32_t kPolDefault = kPolNtInv | kPolBfPick | kPolClampPick;   // measured (cfg4): phase B 80 -> 71 (nt
+// invpos) -> 63.2 us (pick-up); the clamped pick-up: round 117.2-118.8 -> 112.3-112.9 us
 
 // ------------------------------------------------------------------------------ shared pieces
 // Stream [p0, p1) of an index stream: out[p] = lds[idx[p]].  Super-steps of 512 positions per

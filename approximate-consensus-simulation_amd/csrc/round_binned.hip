@@ -272,7 +272,7 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
     constexpr bool FLT = FAULTY || FIX;   // a fault schedule or loss: receiver status and drop mask
     // runs are padded to 16-byte multiples; nrun <= D*kBinSB/16 (checked when the plan is built)
     __shared__ __attribute__((aligned(16)))
-    VT raw[NP > 1 ? kBinPartCap<D, NP> : D * kBinSB + D * kBinSB / 16 * (16 / sizeof(VT) - 1)];
+    VT raw[NP > 1 ? kBinPartCap<D, NP> + 16 / sizeof(VT) : D * kBinSB + D * kBinSB / 16 * (16 / sizeof(VT) - 1)];
     InstState* S = a.st;
     if (S->done) return;
     const uint64_t t0 = a.ts ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -298,8 +298,16 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
     // and issues part 0's DMA before anything else is in flight, so the only wait ahead of the
     // first transfer is the descriptor load itself; later parts issue from registers.
     const bool pf = NP > 1 && nrun <= 64 && !(pol & kPolNoPf);
+    // Clamped pick-up (kPolClampPick; two passes, prefetched descriptors, not the tagged kernels):
+    // part 0 lies END-aligned in the buffer (image position p at raw[p + cap - hi0]) and part 1
+    // start-aligned (p at raw[p - lo1]); raw[cap] holds zeros.  A slot's index, clamped to cap, then
+    // reads its value in its own part and +0 bits in the other, and the two reads are OR-merged: no
+    // compare or select per slot and part.
     uint2 pdsc = make_uint2(0u, 0u);
     uint32_t pnxt = 0;
+    constexpr uint32_t cap = kBinPartCap<D, NP>;
+    const bool clampm = NP == 2 && sizeof(VT) == 8 && !FAULTY && pf && (pol & kPolClampPick);
+    uint32_t hi0 = 0;
     if (pf) {
         const uint32_t lane = threadIdx.x & 63;
         if (lane < nrun) {
@@ -307,7 +315,11 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
             pnxt = tb[lane + 1].y;
         }
         const uint32_t j1 = nrun / NP;
-        bin_dma_runs_pf(pdsc, pnxt, w * j1 / NW, (w + 1) * j1 / NW, stage, raw, 0u);
+        hi0 = __builtin_amdgcn_readlane(pdsc.y, j1);
+        bin_dma_runs_pf(pdsc, pnxt, w * j1 / NW, (w + 1) * j1 / NW, stage, raw, clampm ? hi0 - cap : 0u);
+    }
+    if constexpr (NP > 1) {
+        if (clampm && threadIdx.x < 16 / sizeof(VT)) raw[cap + threadIdx.x] = VT(0);   // +0 bits
     }
     // ordinary loads next (their wait is the barrier's vmcnt(0) anyway)
     const VT xi = live ? reinterpret_cast<const VT*>(a.xin)[i] : VT(0);
@@ -405,6 +417,28 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
         if (a.ts) t1 = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
         for (int t = 0; t < D; ++t) v[1 + t] = raw[pos_of(t)];
+    } else if (sizeof(VT) == 8 && clampm) {
+        const uint32_t lo1 = hi0;
+        // part 0
+        __syncthreads();
+        if (a.ts) t1 = __builtin_amdgcn_s_memrealtime();
+        const uint32_t sh0 = cap - hi0;
+#pragma unroll
+        for (int t = 0; t < D; ++t) {
+            const uint32_t q = pos_of(t) + sh0;
+            v[1 + t] = raw[q < cap ? q : cap];
+        }
+        __syncthreads();   // every lane has read part 0 before part 1 overwrites the buffer's front
+        bin_dma_runs_pf(pdsc, pnxt, nrun / NP + w * (nrun - nrun / NP) / NW, nrun / NP + (w + 1) * (nrun - nrun / NP) / NW,
+                        stage, raw, lo1);
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < D; ++t) {
+            const uint32_t q = pos_of(t) - lo1;   // wraps above cap below lo1
+            const VT u = raw[q < cap ? q : cap];
+            using UB = std::conditional_t<sizeof(VT) == 8, uint64_t, uint32_t>;
+            v[1 + t] = __builtin_bit_cast(VT, (UB)(__builtin_bit_cast(UB, v[1 + t]) | __builtin_bit_cast(UB, u)));
+        }
     } else {
 #pragma unroll
         // Unrolled: the first part skips the p >= lo test and the last part the p < hi test.  This
@@ -1230,7 +1264,7 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     p.ofree = ofree;
     {
         const char* v = getenv("ACSIM_BIN_POL");
-        p.pol = v ? (uint32_t)strtoul(v, nullptr, 0) & 1023u : kPolDefault | (G.levels == 2 ? kPolTwoLevelStores : kPolOneLevelStores);
+        p.pol = v ? (uint32_t)strtoul(v, nullptr, 0) & 2047u : kPolDefault | (G.levels == 2 ? kPolTwoLevelStores : kPolOneLevelStores);
     }
     if (ofree) {   // order-free phase B: receiver ids in image order
         p.rstride = ((uint32_t)d * kBinSB + p.nrun * (G.pad - 1) + 15u) & ~15u;

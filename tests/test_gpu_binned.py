@@ -279,7 +279,7 @@ def test_order_free_f32_and_wmsr(oracle_mod):
             assert np.array_equal(gx.view(np.uint8), o.values(0).view(np.uint8))
 
 
-@pytest.mark.parametrize("name,pol", [("d32_t5_eps_n50000_sa1024", p) for p in (0, 1, 2, 7, 64, 36, 612)] +
+@pytest.mark.parametrize("name,pol", [("d32_t5_eps_n50000_sa1024", p) for p in (0, 1, 2, 7, 64, 36, 612, 1124, 1028)] +
                          [("two_level_d16_t5_n100000_sa256", p) for p in (0, 2, 128, 130, 256, 322)])
 def test_cache_policy_switches_bit_exact(oracle_mod, name, pol):
     """ACSIM_BIN_POL only changes cache policies (nontemporal runs / phase-A and phase-M stage
@@ -290,6 +290,30 @@ def test_cache_policy_switches_bit_exact(oracle_mod, name, pol):
     with oracle_mod.OracleSimulator(cfg, threads=8) as o:
         o.run()
         assert np.array_equal(rb, o.rounds()) and np.array_equal(xb, bits(o.values(0)))
+
+
+@pytest.mark.parametrize("name,pol,pack", [
+    ("d32_t5_eps_n50000_sa1024", 1124, 1), ("d32_t5_eps_n50000_sa1024", 1060, 1),
+    ("d32_t5_eps_n50000_sa1024", 1124, 3), ("d32_t5_dlpsw_sa2048", 1124, 1), ("cfg4_shape_2e17", 1124, 1),
+    ("faulty_d32_t5_byzrandom_drop_sa1024", 1124, 1), ("d32_avg_clean_sa1024", 1124, 1)])
+def test_clamped_pickup_bit_exact(oracle_mod, name, pol, pack):
+    """Clamped two-pass pick-up (ACSIM_BIN_POL bit 1024): part 0 end-aligned in the
+    buffer, part 1 start-aligned, every slot reads its part at an index clamped to a zero slot and
+    the two reads are OR-merged.  Clean, DLPSW, AVERAGE (entry order), packed positions and the fault
+    fix-up kernel, across round(k) calls that end mid-chunk, against the oracle bit for bit."""
+    cfg, sa = CASES[name]
+    with env(ACSIM_BIN_SA=sa, ACSIM_BIN_POL=pol, ACSIM_BIN_PACK=pack):
+        with acsim.Simulator(cfg, device=0) as g:
+            kb = g.kernel_name()
+            g.round(3)
+            g.round(17)
+            g.run()
+            rb, xb, tb = g.rounds(), bits(g.values(0)), bits(g.spread_trace(0))
+    assert " split2" in kb, kb
+    with oracle_mod.OracleSimulator(cfg, threads=8) as o:
+        o.run()
+        assert np.array_equal(rb, o.rounds()) and np.array_equal(xb, bits(o.values(0)))
+        assert np.array_equal(tb, bits(o.spread_trace(0)))
 
 
 @pytest.mark.parametrize("term", ["eps", "fixed"])

@@ -61,6 +61,23 @@ def test_cfg4_full_size_bit_exact(oracle_mod, name, over):
     assert np.array_equal(bits(gt), bits(ot)), "spread traces differ"
 
 
+def test_cfg4_clamped_pickup_matches_golden():
+    """The clamped pick-up (ACSIM_BIN_POL bit 1024 with the one-level default 100) on the bench
+    workload: 100 FIXED rounds against the committed golden hash, bit for bit."""
+    old = os.environ.get("ACSIM_BIN_POL")
+    os.environ["ACSIM_BIN_POL"] = "1124"
+    try:
+        kname, gr, gx, gt = run_gpu(preset("cfg4", max_rounds=100, trace_spread=True))
+    finally:
+        if old is None:
+            os.environ.pop("ACSIM_BIN_POL", None)
+        else:
+            os.environ["ACSIM_BIN_POL"] = old
+    assert " split2" in kname, kname
+    assert int(gr[0]) == 100
+    assert sha256_values(gx) == GOLDEN["cfg4"]["fixed100_x_sha256"]
+
+
 def test_cfg4_f32_fixed100_matches_golden():
     """fp32 mode of the bench workload (100 FIXED rounds) against the oracle-written hash that
     bench.py's cfg4_f32 leg checks."""
