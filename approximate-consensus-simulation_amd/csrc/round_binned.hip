@@ -422,7 +422,10 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
         // part 0
         __syncthreads();
         if (a.ts) t1 = __builtin_amdgcn_s_memrealtime();
-        const uint32_t sh0 = cap - hi0;
+        uint32_t sh0 = cap - hi0;
+        // opaque to the compiler: it otherwise computes (p - lo1) once for both parts, p - lo1 + cap
+        // for part 0 (two VALU instead of one SDWA add) and keeps the 32 differences live across
+        asm volatile("" : "+s"(sh0));
 #pragma unroll
         for (int t = 0; t < D; ++t) {
             const uint32_t q = pos_of(t) + sh0;
