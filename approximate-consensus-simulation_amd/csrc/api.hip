@@ -981,11 +981,13 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     // one or two exchange levels (faults and loss are resolved in phase B from tagged values and
     // slot-order draws); ACSIM_BINNED=0 forces the per-lane kernel and ACSIM_BIN_SA sets the
     // source block size (tests use small blocks on small graphs)
-    // (128 KiB of LDS per phase-A source block: 16 Ki fp64 or 32 Ki fp32 senders)
+    // (128 KiB of LDS per phase-A source block: 16 Ki fp64 or 32 Ki fp32 senders).  Default 16 Ki for
+    // fp32 too: 14-bit packed phase-A indices, and measured faster (cfg4_f32 82.2 -> 80.9 us per round,
+    // cfg5_f32 4.69 -> 4.51 ms; profiles/r04_f32_sa_ab.jsonl); ACSIM_BIN_SA up to 32 Ki
     const uint32_t sa_max = s->f32 ? 32768u : 16384u;
-    uint32_t bin_sa = sa_max;
+    uint32_t bin_sa = 16384u;
     if (const char* v = getenv("ACSIM_BIN_SA")) bin_sa = (uint32_t)strtoul(v, nullptr, 10);
-    if (bin_sa < 64 || bin_sa > sa_max || (bin_sa & (bin_sa - 1))) bin_sa = sa_max;
+    if (bin_sa < 64 || bin_sa > sa_max || (bin_sa & (bin_sa - 1))) bin_sa = 16384u;
     // order-free phase B (clean, sort-based rule: the rows are stored sorted and the rule sees a
     // multiset), ACSIM_BIN_OF=1: measured slower than the invpos phase B, kept as
     // a tested variant

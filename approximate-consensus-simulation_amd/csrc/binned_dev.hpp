@@ -165,7 +165,7 @@ __device__ __forceinline__ void bin_stream(const VT* lx, const uint16_t* __restr
 }
 
 // ------------------------------------------------------------------------------ packed phase-A indices
-// 14-bit packed idxA (fp64 plans, source blocks of at most 16384 senders): the
+// 14-bit packed idxA (source blocks of at most 16384 senders; fp64 and fp32 plans): the
 // stream is cut into blocks of 512 positions (one wave's super-step); block m holds lane l's eight
 // indices — positions 512m + 2(64q + l) + e, index k = 2q + e at bits [14k, 14k + 14) of a 112-bit
 // word — in three u32 planes (words m*224 + 64j + l, j = 0..2: bits 0-95) and one u16 plane
@@ -203,16 +203,18 @@ __device__ __forceinline__ uint32_t pk14_at(const uint32_t* __restrict__ pk, uin
 // waves in turn (wave w takes blocks mb + w, mb + w + NW, ...), software-pipelined like
 // bin_stream_t (the next block's four index loads are issued before this block's gathers and
 // stores); the partial blocks at the ends go position by position.
-template <uint32_t SMODE>
-__device__ __forceinline__ void bin_stream_pk14_t(const double* lx, const uint32_t* __restrict__ pk,
-                                                  double* __restrict__ out, uint64_t p0, uint64_t p1) {
+template <uint32_t SMODE, typename VT = double>
+__device__ __forceinline__ void bin_stream_pk14_t(const VT* lx, const uint32_t* __restrict__ pk,
+                                                  VT* __restrict__ out, uint64_t p0, uint64_t p1) {
+    using V2 = decltype(bin_pair(VT(0), VT(0)));
+    constexpr uint32_t kRebaseBits = sizeof(V2) == 16 ? 27 : 28;   // V2 units per 2 GiB of buffer offsets
     constexpr uint32_t NW = kBinA / 64;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t mb = (p0 + 511) >> 9, me = p1 >> 9;
     if (mb < me) {
         const uint64_t nbw = (me - mb > w) ? (me - mb - w + NW - 1) / NW : 0;   // this wave's blocks
         const uint16_t* pk16 = reinterpret_cast<const uint16_t*>(pk);
-        double2* o2 = reinterpret_cast<double2*>(out);
+        V2* o2 = reinterpret_cast<V2*>(out);
         uint64_t m = mb + w;
         uint32_t c0 = 0, c1 = 0, c2 = 0, ch = 0;
         if (nbw) {
@@ -232,14 +234,15 @@ __device__ __forceinline__ void bin_stream_pk14_t(const double* lx, const uint32
             const uint32_t nh = __builtin_nontemporal_load(pk16 + mn * (2 * kPk14Words) + 384 + lane);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const double2 v = make_double2(lx[pk14_extract(c0, c1, c2, ch, 2 * q)],
-                                               lx[pk14_extract(c0, c1, c2, ch, 2 * q + 1)]);
-                const uint64_t vi = m * 256 + q * 64 + lane;   // double2 index of positions 2vi, 2vi + 1
+                const V2 v = bin_pair(lx[pk14_extract(c0, c1, c2, ch, 2 * q)],
+                                      lx[pk14_extract(c0, c1, c2, ch, 2 * q + 1)]);
+                const uint64_t vi = m * 256 + q * 64 + lane;   // pair index of positions 2vi, 2vi + 1
                 if constexpr (SMODE == 2) {
                     // (buffer offsets are 32-bit: the descriptor is re-based per 2 GiB of stage)
+                    constexpr uint64_t kMask = (1ull << kRebaseBits) - 1;
                     const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-                        o2 + (vi & ~((1ull << 27) - 1)), 0, 0x7FFFFFF0, 0x00020000);
-                    bin_store_sc1(rb, (uint32_t)(vi & ((1ull << 27) - 1)) * 16u, v);
+                        o2 + (vi & ~kMask), 0, 0x7FFFFFF0, 0x00020000);
+                    bin_store_sc1(rb, (uint32_t)(vi & kMask) * (uint32_t)sizeof(V2), v);
                 } else {
                     bin_store(o2 + vi, v, SMODE == 1);
                 }
@@ -257,14 +260,15 @@ __device__ __forceinline__ void bin_stream_pk14_t(const double* lx, const uint32
         for (uint64_t q = (me << 9) + threadIdx.x; q < p1; q += blockDim.x) out[q] = lx[pk14_at(pk, q)];
 }
 
-__device__ __forceinline__ void bin_stream_pk14(const double* lx, const uint32_t* __restrict__ pk, double* __restrict__ out,
+template <typename VT>
+__device__ __forceinline__ void bin_stream_pk14(const VT* lx, const uint32_t* __restrict__ pk, VT* __restrict__ out,
                                                 uint64_t p0, uint64_t p1, uint32_t smode) {
     if (smode == 1)
-        bin_stream_pk14_t<1>(lx, pk, out, p0, p1);
+        bin_stream_pk14_t<1, VT>(lx, pk, out, p0, p1);
     else if (smode == 2)
-        bin_stream_pk14_t<2>(lx, pk, out, p0, p1);
+        bin_stream_pk14_t<2, VT>(lx, pk, out, p0, p1);
     else
-        bin_stream_pk14_t<0>(lx, pk, out, p0, p1);
+        bin_stream_pk14_t<0, VT>(lx, pk, out, p0, p1);
 }
 
 // 14-bit packed phase-B positions (clean fp64 d = 32 plans): per receiver block b, 14 words per lane:

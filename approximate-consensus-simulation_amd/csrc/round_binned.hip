@@ -147,12 +147,10 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
     }
     const uint64_t t1 = ts ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint32_t smode = (pol & kPolSc1Store) ? 2u : (pol & kPolNtStore) ? 1u : 0u;
-    if constexpr (sizeof(VT) == 8) {
-        if (pkA) {   // 14-bit packed indices
-            bin_stream_pk14(lx, pkA, stage, p0, p1, smode);
-            if (ts) bin_ts(ts, t0, t1);
-            return;
-        }
+    if (pkA) {   // 14-bit packed indices
+        bin_stream_pk14(lx, pkA, stage, p0, p1, smode);
+        if (ts) bin_ts(ts, t0, t1);
+        return;
     }
     bin_stream(lx, idxA, stage, p0, p1, smode);
     if (ts) bin_ts(ts, t0, t1);
@@ -1199,7 +1197,7 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     // B keeps the u16 table by default.
     const char* pack_env = getenv("ACSIM_BIN_PACK");
     const uint32_t pack = pack_env ? (uint32_t)strtoul(pack_env, nullptr, 10) : 1u;
-    if (e == hipSuccess && !f32 && sa <= 16384) {
+    if (e == hipSuccess && sa <= 16384) {   // fp64 and fp32 (bit 2 of ACSIM_BIN_PACK: no longer needed)
         if (pack & 1u) {
             const uint64_t nb = (p.Ep1 + 511) / 512;
             e = hipMalloc(&p.pkA, nb * kPk14Words * 4);
@@ -1479,7 +1477,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
         if (phases & 1)
             hipLaunchKernelGGL(k_bin_scatter<float>, dim3((nsrc + 7) / 8 * 8 * p.segs), dim3(kBinA), p.SA * sizeof(float), s,
                                fsrc, p.idxA, p.aoff, st1, a.st, a.N, p.SA, p.segs, p.chunk, pol, fa, fin_on, sel, p.ts, a.eacc,
-                               nullptr);
+                               p.pkA);
         if (p.levels == 2) {
             float* st2 = reinterpret_cast<float*>(p.stage2);
             if (phases & 2)

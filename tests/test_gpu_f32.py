@@ -236,6 +236,39 @@ def test_f32_two_level_matches_oracle(oracle_mod, name):
     assert np.array_equal(tb, to)
 
 
+F32_PACKED = {
+    # (config, ACSIM_BIN_SA): one-level, two-level, tagged (Byzantine + loss), ragged source blocks
+    "d32_t5_n50000_sa1024": (Config(n_nodes=50000, topology="regular", degree=32, rule="trimmed", trim=5,
+                                    eps=1e-6, max_rounds=100, seed=5, trace_spread=True, dtype="f32"), 1024),
+    "d16_t5_n100000_sa256": F32_TWO_LEVEL["d16_t5_n100000_sa256"],
+    "d32_byz_n40000_sa2048": (Config(n_nodes=40000, topology="regular", degree=32, rule="trimmed", trim=5,
+                                     fault_model="byzantine", n_faulty=400, byz_strategy="random", byz_delta=0.1,
+                                     loss_p=0.05, eps=1e-6, max_rounds=100, seed=9, trace_spread=True,
+                                     dtype="f32"), 2048),
+}
+
+
+@pytest.mark.parametrize("name", list(F32_PACKED))
+def test_f32_packed_phase_a_indices_match_oracle(oracle_mod, name):
+    """14-bit packed phase-A indices on fp32 plans (ACSIM_BIN_PACK bit 2 with bit 0):
+    float pairs streamed from the packed stream, write-through and nontemporal stage stores, against
+    the oracle bit for bit, across round(k) calls that end mid-chunk."""
+    cfg, sa = F32_PACKED[name]
+    with _with_env(ACSIM_BIN_SA=sa, ACSIM_BIN_PACK=5), acsim.Simulator(cfg, device=0) as g:
+        kb = g.kernel_name()
+        assert "f32" in kb and "pk14A" in kb, kb
+        g.round(3)
+        g.round(17)
+        g.run()
+        rb, xb, tb = g.rounds(), g.values(0), g.spread_trace(0)
+    with oracle_mod.OracleSimulator(cfg, threads=8) as o:
+        o.run()
+        ro, xo, to = o.rounds(), o.values(0), o.spread_trace(0)
+    assert np.array_equal(rb, ro)
+    assert np.array_equal(xb.view(np.uint32), xo.view(np.uint32)), "packed fp32 values differ from the oracle"
+    assert np.array_equal(tb, to)
+
+
 @pytest.mark.parametrize("parts", [3])
 def test_f32_two_level_virtual_partitions(oracle_mod, parts):
     cfg = Config(n_nodes=100000, topology="regular", degree=16, rule="trimmed", trim=5, eps=1e-6,

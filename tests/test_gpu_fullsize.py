@@ -78,6 +78,25 @@ def test_cfg4_clamped_pickup_matches_golden():
     assert sha256_values(gx) == GOLDEN["cfg4"]["fixed100_x_sha256"]
 
 
+@pytest.mark.parametrize("sa", ["16384"])
+def test_cfg4_f32_packed_matches_golden(sa):
+    """fp32 cfg4 with 14-bit packed phase-A indices (ACSIM_BIN_PACK=5, source blocks of 16 384):
+    100 FIXED rounds against the oracle-written fp32 hash."""
+    old = {k: os.environ.get(k) for k in ("ACSIM_BIN_PACK", "ACSIM_BIN_SA")}
+    os.environ.update(ACSIM_BIN_PACK="5", ACSIM_BIN_SA=sa)
+    try:
+        kname, gr, gx, gt = run_gpu(preset("cfg4", max_rounds=100, dtype="f32", trace_spread=True))
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert "pk14A" in kname, kname
+    assert int(gr[0]) == 100
+    assert sha256_values(gx) == GOLDEN["cfg4"]["f32_fixed100_x_sha256"]
+
+
 def test_cfg4_f32_fixed100_matches_golden():
     """fp32 mode of the bench workload (100 FIXED rounds) against the oracle-written hash that
     bench.py's cfg4_f32 leg checks."""
