@@ -1153,9 +1153,8 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
             if (s->bin.split > 1 && (s->clean || (!s->f32 && s->bin.split == 2)))
                 s->kname += " split" + std::to_string(s->bin.split);
             if (s->bin.ofree) s->kname += " orderfree";
-            if (s->bin.pkA || s->bin.pkinv || s->bin.pkM)   // 14-bit packed index streams
-                s->kname += std::string(" pk14") + (s->bin.pkA ? "A" : "") + (s->bin.pkM ? "M" : "") +
-                            (s->bin.pkinv ? "B" : "");
+            if (s->bin.pkA || s->bin.pkinv)   // 14-bit packed index streams
+                s->kname += std::string(" pk14") + (s->bin.pkA ? "A" : "") + (s->bin.pkinv ? "B" : "");
             if (s->bin.fix) {   // fault fix-up list instead of tagged senders
                 const size_t pos = s->kname.find("+k_bin_tag");
                 if (pos != std::string::npos) s->kname.replace(pos, 10, "+k_bin_fixup");

@@ -173,7 +173,6 @@ struct BinnedPlan {
     uint16_t* idxA = nullptr;           // [Ep1] sender index within its source block (0 in pads)
     uint32_t* pkA = nullptr;            // idxA packed to 14 bits (binned_dev.hpp pk14; fp64, SA <= 16384), idxA then freed
     uint16_t* idxM = nullptr;           // [Ep2] position inside the phase-M LDS image (two levels)
-    uint32_t* pkM = nullptr;            // idxM packed to 14 bits (ACSIM_BIN_PACK bit 3; images of <= 16384 entries)
     uint16_t* invpos = nullptr;         // [Q][D/8][kBinSB][8]: position of (receiver, slot) in block b's runs
     uint32_t* pkinv = nullptr;          // invpos packed to 14 bits (clean fp64 d = 32 two-pass plans; binned_dev.hpp)
     uint2* tiles = nullptr;             // [Q][nrun+1] (stage start | pad count, element offset in block b's runs)

@@ -164,7 +164,7 @@ template <typename VT = double>
 __global__ __launch_bounds__(kBinA) void k_bin_regroup(const VT* __restrict__ stage1, const uint2* __restrict__ mt,
                                                      const uint64_t* __restrict__ moff, const uint16_t* __restrict__ idxM,
                                                      VT* __restrict__ stage2, const InstState* __restrict__ st,
-                                                     uint32_t PK, uint32_t pol, const uint32_t* __restrict__ pkM) {
+                                                     uint32_t PK, uint32_t pol) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lm_raw[];
     VT* lm = reinterpret_cast<VT*>(lm_raw);
     if (st->done) return;
@@ -173,11 +173,7 @@ __global__ __launch_bounds__(kBinA) void k_bin_regroup(const VT* __restrict__ st
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     bin_dma_runs(mt + (uint64_t)g * (PK + 1), w * PK / NW, (w + 1) * PK / NW, stage1, lm);
     __syncthreads();
-    const uint32_t smode = (pol & kPolSc1StoreM) ? 2u : (pol & kPolNtStoreM) ? 1u : 0u;
-    if (pkM)   // 14-bit packed image positions
-        bin_stream_pk14(lm, pkM, stage2, moff[g], moff[g + 1], smode);
-    else
-        bin_stream(lm, idxM, stage2, moff[g], moff[g + 1], smode);
+    bin_stream(lm, idxM, stage2, moff[g], moff[g + 1], (pol & kPolSc1StoreM) ? 2u : (pol & kPolNtStoreM) ? 1u : 0u);
 }
 
 // ------------------------------------------------------------------------------ phase B
@@ -1053,7 +1049,6 @@ void binned_free(BinnedPlan& p) {
     (void)hipFree(p.pkA);
     (void)hipFree(p.pkinv);
     (void)hipFree(p.idxM);
-    (void)hipFree(p.pkM);
     (void)hipFree(p.invpos);
     (void)hipFree(p.rid);
     (void)hipFree(p.tiles);
@@ -1258,21 +1253,6 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
         (void)hipFree(lpos);
         (void)hipFree(cap);
         last = &T2;
-        // 14-bit packed phase-M positions (ACSIM_BIN_PACK bit 3) when every image holds <= 2^14 entries
-        if (e == hipSuccess && (pack & 8u) && p.mcap <= 16384) {
-            const uint64_t nb = (p.Ep2 + 511) / 512;
-            e = hipMalloc(&p.pkM, nb * kPk14Words * 4);
-            if (e == hipSuccess) {
-                hipLaunchKernelGGL(k_bin_pack14, dim3((unsigned)((nb * 64 + 255) / 256)), dim3(256), 0, s, p.idxM, p.Ep2,
-                                   p.pkM);
-                e = hipGetLastError();
-            }
-            if (e == hipSuccess) e = hipStreamSynchronize(s);
-            if (e == hipSuccess) {
-                (void)hipFree(p.idxM);
-                p.idxM = nullptr;
-            }
-        }
     }
     // ---- phase B tables over the last stage
     const uint64_t Qp = (uint64_t)G.Q * kBinSB;   // receiver slots incl. the ragged last block's padding
@@ -1502,7 +1482,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
             float* st2 = reinterpret_cast<float*>(p.stage2);
             if (phases & 2)
                 hipLaunchKernelGGL(k_bin_regroup<float>, dim3(p.ngroups), dim3(kBinA), (p.mcap + 4) * sizeof(float), s, st1,
-                                   p.mt, p.moff, p.idxM, st2, a.st, p.PK, pol, p.pkM);
+                                   p.mt, p.moff, p.idxM, st2, a.st, p.PK, pol);
             st1 = st2;   // phase B reads the regrouped stage
         }
         if (fixp)
@@ -1564,7 +1544,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
     if (p.levels == 2) {
         if (phases & 2)
             hipLaunchKernelGGL(k_bin_regroup<double>, dim3(p.ngroups), dim3(kBinA), (p.mcap + 2) * sizeof(double), s,
-                               p.stage1, p.mt, p.moff, p.idxM, p.stage2, a.st, p.PK, pol, p.pkM);
+                               p.stage1, p.mt, p.moff, p.idxM, p.stage2, a.st, p.PK, pol);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         last = p.stage2;
     }

@@ -380,26 +380,6 @@ def test_packed_index_streams_bit_exact(oracle_mod, pack):
             assert np.array_equal(tb, bits(o.spread_trace(0)))
 
 
-@pytest.mark.parametrize("name", ["two_level_d16_t5_n100000_sa256", "d8_t2_midpoint_sa256"])
-def test_packed_phase_m_positions_bit_exact(oracle_mod, name):
-    """14-bit packed phase-M image positions (ACSIM_BIN_PACK bit 3, two-level plans whose images
-    hold <= 2^14 entries: 12 Ki-delivery image target) against the oracle, stepped
-    round(k) calls included."""
-    cfg, sa = CASES[name]
-    with env(ACSIM_BIN_SA=sa, ACSIM_BIN_PACK=9, ACSIM_BIN_MIMG=12288):
-        with acsim.Simulator(cfg, device=0) as g:
-            kb = g.kernel_name()
-            g.round(3)
-            g.round(17)
-            g.run()
-            rb, xb, tb = g.rounds(), bits(g.values(0)), bits(g.spread_trace(0))
-    assert "k_bin_regroup" in kb and "pk14AM" in kb, kb
-    with oracle_mod.OracleSimulator(cfg, threads=8) as o:
-        o.run()
-        assert np.array_equal(rb, o.rounds()) and np.array_equal(xb, bits(o.values(0)))
-        assert np.array_equal(tb, bits(o.spread_trace(0)))
-
-
 @pytest.mark.parametrize("variant", ["split2", "order_free", "fixup", "var"])
 def test_eps_publication_in_every_gather_variant(oracle_mod, variant):
     """Every phase-B kernel that writes a binned round's partials publishes its (min, max) for the

@@ -159,31 +159,6 @@ def test_cfg5_full_size_matches_golden():
     assert np.all(np.diff(tr) <= 0)
 
 
-@pytest.mark.parametrize("mimg", ["14336", "16384"])
-def test_cfg5_packed_phase_m_matches_golden(mimg):
-    """cfg5 with 14-bit packed phase-M positions (ACSIM_BIN_PACK bit 3): x^10 hashes to
-    the oracle's.  At the default image target some images exceed 2^14 entries and the plan keeps
-    the u16 positions; at 14 Ki every image fits and the packed stream runs."""
-    old = {k: os.environ.get(k) for k in ("ACSIM_BIN_PACK", "ACSIM_BIN_MIMG")}
-    os.environ.update(ACSIM_BIN_PACK="9", ACSIM_BIN_MIMG=mimg)
-    try:
-        cfg = preset("cfg5", max_rounds=10, trace_spread=True)
-        with acsim.Simulator(cfg, device=0) as s:
-            kname = s.kernel_name()
-            s.round(10)
-            x = s.values(0)
-            assert sha256_values(x) == GOLDEN["cfg5"]["x10_sha256"]
-            assert [float(v).hex() for v in s.spread_trace(0)] == GOLDEN["cfg5"]["trace"]
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-    if mimg == "14336":
-        assert "pk14AM" in kname, kname
-
-
 def test_cfg5_full_size_eight_virtual_partitions():
     """The 8-GPU data flow of cfg5 (rows split in 8 blocks, each partition reading only its own
     copy of x, an all-gather after every round) on one device at full size: every private copy
