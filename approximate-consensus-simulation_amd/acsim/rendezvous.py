@@ -61,8 +61,11 @@ def _recv(sock: socket.socket) -> Any:
     return msgpack.unpackb(_recv_exact(sock, n), raw=False)
 
 
-def _is_local(addr: str) -> bool:
-    return addr == "localhost" or addr.startswith("127.")
+def _bind_addr(addr: str) -> str:
+    """The address rank 0 listens on: the one the other ranks connect to.  "localhost" becomes
+    127.0.0.1; any other name or literal (127.0.1.1, Debian's hostname mapping, included) is bound
+    as given, so a loopback address other than 127.0.0.1 is reachable too."""
+    return "127.0.0.1" if addr == "localhost" else addr
 
 
 class Group:
@@ -83,7 +86,7 @@ class Group:
             srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
             srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
             try:
-                srv.bind(("127.0.0.1" if _is_local(addr) else addr, port))
+                srv.bind((_bind_addr(addr), port))
             except OSError as e:
                 srv.close()
                 raise ConnectionError(

@@ -207,7 +207,10 @@ template <uint32_t SMODE, typename VT = double>
 __device__ __forceinline__ void bin_stream_pk14_t(const VT* lx, const uint32_t* __restrict__ pk,
                                                   VT* __restrict__ out, uint64_t p0, uint64_t p1) {
     using V2 = decltype(bin_pair(VT(0), VT(0)));
-    constexpr uint32_t kRebaseBits = sizeof(V2) == 16 ? 27 : 28;   // V2 units per 2 GiB of buffer offsets
+    // V2 units per 1 GiB window: the descriptor's num_records (0x7FFFFFF0) must cover the whole window
+    // plus one V2 (with 2 GiB windows the last pair of each window sat at offset 0x7FFFFFF0 and its
+    // store failed the range check silently; stages above 2 GiB are two-level, cfg5-sized plans)
+    constexpr uint32_t kRebaseBits = sizeof(V2) == 16 ? 26 : 27;
     constexpr uint32_t NW = kBinA / 64;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t mb = (p0 + 511) >> 9, me = p1 >> 9;
@@ -238,7 +241,7 @@ __device__ __forceinline__ void bin_stream_pk14_t(const VT* lx, const uint32_t* 
                                       lx[pk14_extract(c0, c1, c2, ch, 2 * q + 1)]);
                 const uint64_t vi = m * 256 + q * 64 + lane;   // pair index of positions 2vi, 2vi + 1
                 if constexpr (SMODE == 2) {
-                    // (buffer offsets are 32-bit: the descriptor is re-based per 2 GiB of stage)
+                    // (buffer offsets are 32-bit: the descriptor is re-based per 1 GiB of stage)
                     constexpr uint64_t kMask = (1ull << kRebaseBits) - 1;
                     const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
                         o2 + (vi & ~kMask), 0, 0x7FFFFFF0, 0x00020000);
@@ -270,11 +273,6 @@ __device__ __forceinline__ void bin_stream_pk14(const VT* lx, const uint32_t* __
     else
         bin_stream_pk14_t<0, VT>(lx, pk, out, p0, p1);
 }
-
-// 14-bit packed phase-B positions (clean fp64 d = 32 plans): per receiver block b, 14 words per lane:
-// words 0-11 as three uint4 planes [b][j][256 lanes], words 12-13 as one uint2 plane [b][256]; slot t's
-// position at bits [14t, 14t + 14) of the lane's 448 bits.  14 KiB per block instead of 16.
-constexpr uint32_t kPk14InvWords = 14 * kBinSB;   // u32 words per receiver block
 
 // Copy runs [r0, r1) of a run table (start in `src` elements, element offset `pre` in the LDS
 // image; run k ends where run k+1's image begins) into LDS by 16-byte LDS-DMA.  Every run is

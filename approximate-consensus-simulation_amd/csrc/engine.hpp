@@ -134,16 +134,20 @@ hipError_t build_fault_status(uint32_t* status, uint64_t B, uint64_t N, uint32_t
 hipError_t launch_partials_from_x(const double* x, const uint32_t* status, uint64_t B, uint64_t N,
                                   double2* partial, uint32_t nblk, bool f32, hipStream_t s);
 hipError_t launch_finalize(const FinalizeArgs& a, uint64_t B, hipStream_t s);
-struct RunSummary {   // acs_run's result, folded on the device (32 bytes)
+struct RunSummary {   // acs_run's result, folded on the device (40 bytes)
     unsigned int rounds_max, n_done;   // n_done: instances whose done flag is set
     unsigned long long n_converged, rounds_sum, spread_max_bits;
+    unsigned long long seq;            // stored last (system-scope release): the launch's sequence number
 };
 // acs_run's summary in ONE launch with no copy: block partials, then the last block to arrive folds
 // them and stores the summary (with the count of done instances) straight into host-mapped memory
 // `out`.  scratch: a device buffer of kSummaryScratch bytes whose first word is zero (the last block
-// re-zeroes it).
+// re-zeroes it).  The summary's fields land before `seq` (a system-scope release store of the
+// launch's sequence number), so the host may read them once it sees `seq` without waiting for the
+// stream's completion signal.
 constexpr uint32_t kSummaryScratch = 1024 * 48 + 64;
-hipError_t launch_run_summary_mapped(const InstState* st, uint64_t B, void* scratch, RunSummary* out, hipStream_t s);
+hipError_t launch_run_summary_mapped(const InstState* st, uint64_t B, void* scratch, RunSummary* out,
+                                     unsigned long long seq, hipStream_t s);
 
 // ---- round kernels
 // Register-resident kernel for RANDOM_REGULAR with a compiled (d, t) pair; returns
@@ -174,7 +178,6 @@ struct BinnedPlan {
     uint32_t* pkA = nullptr;            // idxA packed to 14 bits (binned_dev.hpp pk14; fp64, SA <= 16384), idxA then freed
     uint16_t* idxM = nullptr;           // [Ep2] position inside the phase-M LDS image (two levels)
     uint16_t* invpos = nullptr;         // [Q][D/8][kBinSB][8]: position of (receiver, slot) in block b's runs
-    uint32_t* pkinv = nullptr;          // invpos packed to 14 bits (clean fp64 d = 32 two-pass plans; binned_dev.hpp)
     uint2* tiles = nullptr;             // [Q][nrun+1] (stage start | pad count, element offset in block b's runs)
     bool ofree = false;                 // order-free phase B (rid, no invpos)
     bool var = false;                   // CSR rows below the compiled degree (kEllNone columns)

@@ -48,7 +48,8 @@ struct SumPart {
     uint32_t ndone, pad;
 };
 __global__ __launch_bounds__(kReduceBlock) void k_run_summary_mapped(const InstState* __restrict__ st, uint64_t B,
-                                                                     unsigned char* scratch, RunSummary* out) {
+                                                                     unsigned char* scratch, RunSummary* out,
+                                                                     unsigned long long seq) {
     uint32_t* cnt = reinterpret_cast<uint32_t*>(scratch);
     SumPart* part = reinterpret_cast<SumPart*>(scratch + 64);
     __shared__ SumPart red[kReduceBlock / 64];
@@ -119,14 +120,17 @@ __global__ __launch_bounds__(kReduceBlock) void k_run_summary_mapped(const InstS
         out->rounds_sum = rsum;
         out->spread_max_bits = smax;
         *cnt = 0;   // ready for the next launch (stream-ordered)
+        // last: the sequence number, released at system scope after the fields above (the host polls it)
+        __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
-hipError_t launch_run_summary_mapped(const InstState* st, uint64_t B, void* scratch, RunSummary* out, hipStream_t s) {
+hipError_t launch_run_summary_mapped(const InstState* st, uint64_t B, void* scratch, RunSummary* out,
+                                     unsigned long long seq, hipStream_t s) {
     const uint64_t g = (B + kReduceBlock - 1) / kReduceBlock;
     static_assert(64 + 1024 * sizeof(SumPart) <= kSummaryScratch, "summary scratch");
     hipLaunchKernelGGL(k_run_summary_mapped, dim3((unsigned)(g == 0 ? 1 : g < 1024 ? g : 1024)), dim3(kReduceBlock), 0, s,
-                       st, B, reinterpret_cast<unsigned char*>(scratch), out);
+                       st, B, reinterpret_cast<unsigned char*>(scratch), out, seq);
     return hipGetLastError();
 }
 

@@ -256,16 +256,13 @@ __global__ __launch_bounds__(256) void k_bin_fixup(const uint4* __restrict__ fix
 // delivery (k_bin_fixup), a missing one as a quiet NaN; phase B draws the §A.5 drop mask, turns
 // dropped and NaN entries into missing ones and applies the receiver's own status — no tag
 // decoding, no Byzantine draws, clean-kernel registers.
-// PK14 (clean d = 32 plans): `invpos` points at the 14-bit packed positions
-// (binned_dev.hpp pk14inv layout) instead of the u16 table.
 template <int D, int T, bool WMSR = false, bool FAULTY = false, typename VT = double, int NP = 1, bool VAR = false,
-          bool FIX = false, bool PK14 = false>
+          bool FIX = false>
 __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) : FIX && NP > 1 && (T || WMSR) ? 4 : 1) void k_bin_gather(const RoundArgs a, const VT* __restrict__ stage,
                                                        const uint16_t* __restrict__ invpos,
                                                        const uint2* __restrict__ tiles, uint32_t nrun, uint32_t Q,
                                                        uint32_t Qc, uint32_t pol) {
     static_assert(D % 8 == 0, "invpos is read 8 slots at a time");
-    static_assert(!PK14 || (D == 32 && !FAULTY && !FIX && !VAR), "packed positions: clean d = 32 plans");
     static_assert(!(FIX && FAULTY), "FIX replaces the tagged resolution");
     constexpr bool FLT = FAULTY || FIX;   // a fault schedule or loss: receiver status and drop mask
     // runs are padded to 16-byte multiples; nrun <= D*kBinSB/16 (checked when the plan is built)
@@ -364,39 +361,14 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
         }
     }
     uint4 ip[D / 8];
-    uint32_t pw[PK14 ? 14 : 1];   // packed: the lane's 32 positions at bits [14t, 14t + 14)
-    if constexpr (PK14) {
-        const uint32_t* bb = reinterpret_cast<const uint32_t*>(invpos) + (uint64_t)b * kPk14InvWords;
-        using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
-        using u32x2 = unsigned int __attribute__((ext_vector_type(2)));
-        const u32x4* p4 = reinterpret_cast<const u32x4*>(bb) + threadIdx.x;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            const u32x4 t4 = __builtin_nontemporal_load(p4 + j * kBinSB);
-            pw[4 * j] = t4.x;
-            pw[4 * j + 1] = t4.y;
-            pw[4 * j + 2] = t4.z;
-            pw[4 * j + 3] = t4.w;
-        }
-        const u32x2 t2 = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(bb + 3 * 4 * kBinSB) + threadIdx.x);
-        pw[12] = t2.x;
-        pw[13] = t2.y;
-    }
     // position of slot t (compile-time t)
     auto pos_of = [&](int t) -> uint32_t {
-        if constexpr (PK14) {
-            const int bit = 14 * t, wi = bit >> 5, sh = bit & 31;
-            if (sh + 14 <= 32) return __builtin_amdgcn_ubfe(pw[wi], sh, 14);
-            return __builtin_amdgcn_alignbit(pw[wi + 1], pw[wi], sh) & 0x3FFFu;
-        } else {
-            const uint4& u = ip[t / 8];
-            const uint32_t wd = (t & 6) == 0 ? u.x : (t & 6) == 2 ? u.y : (t & 6) == 4 ? u.z : u.w;
-            return (t & 1) ? wd >> 16 : wd & 0xFFFFu;
-        }
+        const uint4& u = ip[t / 8];
+        const uint32_t wd = (t & 6) == 0 ? u.x : (t & 6) == 2 ? u.y : (t & 6) == 4 ? u.z : u.w;
+        return (t & 1) ? wd >> 16 : wd & 0xFFFFu;
     };
     const uint4* ipp = reinterpret_cast<const uint4*>(invpos) + (uint64_t)b * (D / 8) * kBinSB + threadIdx.x;
-    if constexpr (PK14) {
-    } else if (pol & kPolNtInv) {
+    if (pol & kPolNtInv) {
         using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
         const u32x4* ipn = reinterpret_cast<const u32x4*>(ipp);
 #pragma unroll
@@ -842,24 +814,6 @@ __global__ __launch_bounds__(256) void k_bin_pack14(const uint16_t* __restrict__
     reinterpret_cast<uint16_t*>(pk)[m * (2 * kPk14Words) + 384 + l] = (uint16_t)(acc[1] >> 32);
 }
 
-// invpos (d = 32) -> 14-bit packed positions (binned_dev.hpp kPk14InvWords layout): workgroup = block b,
-// lane = receiver
-__global__ __launch_bounds__(kBinSB) void k_bin_pack14inv(const uint16_t* __restrict__ invpos, uint32_t* __restrict__ pk) {
-    constexpr uint32_t D = 32;
-    const uint32_t b = blockIdx.x, l = threadIdx.x;
-    uint32_t w[14] = {};
-    for (uint32_t t = 0; t < D; ++t) {
-        const uint32_t v = invpos[(((uint64_t)b * (D / 8) + t / 8) * kBinSB + l) * 8 + (t & 7)] & 0x3FFFu;
-        const uint32_t bit = 14 * t, wi = bit >> 5, sh = bit & 31;
-        w[wi] |= v << sh;
-        if (sh + 14 > 32) w[wi + 1] |= v >> (32 - sh);
-    }
-    uint32_t* bb = pk + (uint64_t)b * kPk14InvWords;
-    for (uint32_t j = 0; j < 3; ++j)
-        for (uint32_t c = 0; c < 4; ++c) bb[(j * kBinSB + l) * 4 + c] = w[4 * j + c];
-    bb[3 * 4 * kBinSB + 2 * l] = w[12];
-    bb[3 * 4 * kBinSB + 2 * l + 1] = w[13];
-}
 
 // phase-A ranges: aoff[a] = padded start of source block a's deliveries (aoff[P] = Ep)
 __global__ __launch_bounds__(256) void k_bin_aoff(const uint32_t* __restrict__ pstart, uint32_t P, uint32_t G1,
@@ -1047,7 +1001,6 @@ void binned_free(BinnedPlan& p) {
     }
     (void)hipFree(p.idxA);
     (void)hipFree(p.pkA);
-    (void)hipFree(p.pkinv);
     (void)hipFree(p.idxM);
     (void)hipFree(p.invpos);
     (void)hipFree(p.rid);
@@ -1191,10 +1144,10 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
         e = hipGetLastError();
     }
     // 14-bit packed phase-A indices (fp64 plans with source blocks of at most 2^14 senders).
-    // ACSIM_BIN_PACK: bit 0 phase A, bit 1 phase B (default 1; 0: u16 streams).  Measured per kernel
-    // (rocprofv3, cfg4, profiles/r04_s8_pack_kernel_stats.csv): packed idxA 59.4 -> 53-54 us;
-    // packed invpos 61.7-61.8 -> 62.5-63.0 us (phase B's decode costs more than its 8 MB), so phase
-    // B keeps the u16 table by default.
+    // ACSIM_BIN_PACK: bit 0 (default 1; 0: u16 stream).  Measured per kernel (rocprofv3, cfg4,
+    // profiles/r04_s8_pack_kernel_stats.csv): packed idxA 59.4 -> 53-54 us.  Packed phase-B
+    // positions measured slower (62.5-63.0 against 61.7-61.8 us: the decode sits on phase B's
+    // critical path) and were removed in round 5 (history: d8efbd1).
     const char* pack_env = getenv("ACSIM_BIN_PACK");
     const uint32_t pack = pack_env ? (uint32_t)strtoul(pack_env, nullptr, 10) : 1u;
     if (e == hipSuccess && sa <= 16384) {   // fp64 and fp32 (bit 2 of ACSIM_BIN_PACK: no longer needed)
@@ -1342,26 +1295,6 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
                     fits = row[(k + 1) * p.nrun / np].y - row[k * p.nrun / np].y <= cap;
             }
             if (fits) p.split = np;
-            // 14-bit packed positions for phase B: clean fp64 d = 32 two-pass
-            // plans whose every block image holds fewer than 2^14 entries
-            uint32_t mxpos = 0;
-            for (uint32_t b = 0; b < G.Q; ++b) {
-                const uint32_t tot = h[(uint64_t)b * (p.nrun + 1) + p.nrun].y;
-                mxpos = tot > mxpos ? tot : mxpos;
-            }
-            if (e == hipSuccess && p.split == 2 && clean && !tagged && !f32 && !var && D == 32 && mxpos <= 16384 &&
-                (pack & 2u)) {
-                e = hipMalloc(&p.pkinv, (uint64_t)G.Q * kPk14InvWords * 4);
-                if (e == hipSuccess) {
-                    hipLaunchKernelGGL(k_bin_pack14inv, dim3(G.Q), dim3(kBinSB), 0, s, p.invpos, p.pkinv);
-                    e = hipGetLastError();
-                }
-                if (e == hipSuccess) e = hipStreamSynchronize(s);
-                if (e == hipSuccess) {
-                    (void)hipFree(p.invpos);
-                    p.invpos = nullptr;
-                }
-            }
         }
     }
     // phase-A segmentation: for few source blocks about 256 workgroups per launch (one generation: one 128 KiB-LDS
@@ -1430,12 +1363,7 @@ static hipError_t binned_set_lds_attributes() {
 // clean phase B in p.split (2..4) passes
 #define ACS_BIN_NP_LAUNCH(DD, TT, W, VT_, SRC)                                                         \
     {                                                                                                  \
-        if (p.split == 2 && p.pkinv) {                                                                 \
-            if constexpr (DD == 32 && sizeof(VT_) == 8)                                                    \
-                hipLaunchKernelGGL((k_bin_gather<DD, TT, W, false, VT_, 2, false, false, true>), grid,     \
-                                   dim3(kBinSB), 0, s, a, SRC, reinterpret_cast<const uint16_t*>(p.pkinv), \
-                                   p.tiles, p.nrun, p.Q, Qc, pol);                                        \
-        } else if (p.split == 2)                                                                       \
+        if (p.split == 2)                                                                              \
             hipLaunchKernelGGL((k_bin_gather<DD, TT, W, false, VT_, 2>), grid, dim3(kBinSB), 0, s, a, SRC, \
                                p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                  \
         else if (p.split == 3)                                                                         \

@@ -32,14 +32,16 @@ the headline line; a watchdog prints the line if a leg hangs):
                     100 FIXED rounds of a fresh handle checked against the oracle's hash.
   cfg3_sharded      10^5 instances x 64 nodes (BASELINE configs[2]) sharded over the ranks by
                     contiguous global instance blocks, no data-path collective; node-rounds/s
-                    of the whole job (the batch run 4 times back to back per rank, so the
-                    fixed per-rank cost is amortised alike at every N), and the checksum of
-                    per-instance checksums gathered on rank 0 compared with
-                    tests/golden/fullsize.json (every repetition must agree).
-  cfg5_partitioned  N = 2^26 random 16-regular (BASELINE configs[4]) node-partitioned over the
-                    ranks with a per-round RCCL all-gather (one plain handle at N = 1); W warm-up
-                    + R timed FIXED rounds, ms/round, the all-gather share, and sha256(x) after
-                    the 10 rounds against the golden hash.
+                    of the whole job (the batch run 8 times back to back per rank, so the
+                    fixed per-rank cost is amortised alike at every N; `single` times one
+                    unamortised run), and the checksum of per-instance checksums gathered on
+                    rank 0 compared with tests/golden/fullsize.json (every repetition must agree).
+  cfg5_partitioned  N = 2^26 random 16-regular (BASELINE configs[4]); one plain handle at N = 1,
+                    node-partitioned over the ranks at N > 1, where BOTH exchange sequences run on
+                    their own handles (the per-round RCCL all-gather, the default, and the chunked
+                    send / receive with ACSIM_XCHUNKS=4); W warm-up + R timed FIXED rounds,
+                    ms/round, the exchange share, and sha256(x) after the 10 rounds against the
+                    golden hash, per sequence.
 """
 from __future__ import annotations
 
@@ -77,8 +79,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--dtype", default="f64", choices=["f64", "f32"],
                    help="value type; the headline is fp64, fp32 mode (DESIGN.md §9) is reported separately")
-    p.add_argument("--cpu-seconds", type=float, default=12.0,
-                   help="target CPU work for the bounded cpu_baseline sample")
+    p.add_argument("--cpu-seconds", type=float, default=20.0,
+                   help="target CPU time of the two bounded cpu_baseline samples together (1 thread, all cores)")
     p.add_argument("--no-event-timing", action="store_true",
                    help="skip per-launch HIP events (roofline then uses ms_per_step)")
     p.add_argument("--event-run", type=int, default=25,
@@ -94,13 +96,44 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(n_nodes: int, seconds: float, dtype: str = "f64") -> dict:
-    """Time the oracle (oracle/acs_oracle.c, -O2, OpenMP over receivers) on the host cores."""
+def host_facts() -> dict:
+    """nproc, the CPUs this process may run on, and the CPU model (the CPU timing
+    records the host it ran on)."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    return {"nproc": os.cpu_count(), "affinity_cpus": affinity, "cpu_model": model,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+
+
+def all_core_threads() -> tuple:
+    """The all-core thread count and why: OMP_NUM_THREADS when set (the GPU box sets it to the
+    job's CPU share, 16 threads per GPU, while nproc there counts the whole machine), else the
+    CPUs this process may run on."""
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if env > 0:
+        return env, "OMP_NUM_THREADS (the job's CPU share on the GPU box)"
+    try:
+        return max(1, len(os.sched_getaffinity(0))), "sched_getaffinity"
+    except (AttributeError, OSError):
+        return max(1, os.cpu_count() or 1), "os.cpu_count()"
+
+
+def time_oracle(n_nodes: int, seconds: float, dtype: str, threads: int) -> dict:
+    """One bounded sample of the oracle on the cfg4 workload: a warm-up round, then as many FIXED
+    rounds as fit in about `seconds`."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from acsim import preset
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, 16))
     cfg = preset("cfg4", n_nodes=n_nodes, max_rounds=10000, omp_threads=threads, dtype=dtype)
     with O.OracleSimulator(cfg, threads=threads) as o:
         t0 = time.perf_counter()
@@ -110,10 +143,23 @@ def cpu_baseline(n_nodes: int, seconds: float, dtype: str = "f64") -> dict:
         t0 = time.perf_counter()
         o.round(rounds)
         dt = time.perf_counter() - t0
-    return {"value": n_nodes * rounds / dt, "unit": "node-rounds/s", "cores": threads,
+    return {"value": n_nodes * rounds / dt, "threads": threads, "rounds": rounds, "seconds": dt}
+
+
+def cpu_baseline(n_nodes: int, seconds: float, dtype: str = "f64") -> dict:
+    """Time the oracle (oracle/acs_oracle.c, -O2, OpenMP over receivers) on the host, single-threaded
+    and on all the job's cores, each on a bounded sample of the same workload.
+    `value` / `cores` are the all-core figure."""
+    t_all, why = all_core_threads()
+    one = time_oracle(n_nodes, seconds / 2, dtype, 1)
+    allc = time_oracle(n_nodes, seconds / 2, dtype, t_all)
+    return {"value": allc["value"], "unit": "node-rounds/s", "cores": t_all,
             "kind": "port",
-            "sample": f"cfg4 (N={n_nodes}, d=32, t=5, FIXED) — {rounds} rounds after 1 warm-up "
-                      f"round, {dt:.1f} s, oracle/acs_oracle.c with {threads} OpenMP threads"}
+            "sample": f"cfg4 (N={n_nodes}, d=32, t=5, FIXED, {dtype}) — oracle/acs_oracle.c: "
+                      f"{one['rounds']} rounds on 1 thread ({one['seconds']:.1f} s) and {allc['rounds']} rounds "
+                      f"on {t_all} OpenMP threads ({allc['seconds']:.1f} s), each after 1 warm-up round",
+            "threads_1": one, "threads_all": dict(allc, source=why),
+            "host": host_facts()}
 
 
 def lib_sha256() -> str:
@@ -215,13 +261,16 @@ def golden():
 
 
 def leg_cfg3(ctx: Ctx, reps: int = 8) -> dict:
-    """BASELINE configs[2]: instance sharding, no data-path collective.  The timed
-    region runs the rank's shard `reps` times back to back (one handle each, created before it), so
-    the per-rank fixed cost (launch, the end-of-run sync) is amortised the same way at every N;
-    every handle's checksum of per-instance checksums is checked.  `value` is the job's makespan
-    rate: all node-rounds over the slowest rank's time from the common start barrier to its last
-    run's return (the closing barrier over the socket control plane — tens of µs per collective at
-    N = 8, none at N = 1 — only aligns the ranks; `seconds` keeps the time through it)."""
+    """BASELINE configs[2]: instance sharding, no data-path collective.  Two timed
+    regions, each from a common start barrier to the slowest rank's last run() return:
+      - `single`: ONE run() of the rank's shard on a fresh handle — the unamortised makespan of the
+        job, fixed per-rank cost (launch, summary, wake-up) included;
+      - the main figure: the shard run `reps` times back to back (one handle each, all created
+        before it), so the per-rank fixed cost is amortised the same way at every N.
+    Every handle's checksum of per-instance checksums is checked.  `value` is the amortised
+    makespan rate: all node-rounds over the slowest rank's time (the closing barrier over the
+    socket control plane — tens of µs per collective at N = 8, none at N = 1 — only aligns the
+    ranks; `seconds` keeps the time through it)."""
     import numpy as np
     import acsim
     from acsim.digest import instance_digests, combine_digests
@@ -234,6 +283,7 @@ def leg_cfg3(ctx: Ctx, reps: int = 8) -> dict:
     try:
         with acsim.Simulator(local.replace(n_instances=min(256, max(cnt, 1))), device=ctx.dev) as w:
             w.run()   # code-object load and first launch outside the timed region
+        one = acsim.Simulator(local, device=ctx.dev)   # the single-run figure: no kernel events
         for _ in range(reps):
             sims.append(acsim.Simulator(local, device=ctx.dev))
             sims[-1].set_kernel_timing(True)
@@ -241,6 +291,13 @@ def leg_cfg3(ctx: Ctx, reps: int = 8) -> dict:
         err = f"{type(e).__name__}: {e}"
     if not ctx.all_ok(err is None):
         raise RuntimeError(err or "another rank failed to create its cfg3 shard")
+    ctx.barrier(one)
+    t0 = time.perf_counter()
+    one.run()
+    t_one = ctx.max(time.perf_counter() - t0)
+    one_rounds = one.rounds()
+    one_dig = instance_digests(one.all_values())
+    one.close()
     ctx.barrier(sims[0])
     t0 = time.perf_counter()
     for sim in sims:
@@ -254,6 +311,7 @@ def leg_cfg3(ctx: Ctx, reps: int = 8) -> dict:
     rounds = sims[0].rounds()
     digs = [instance_digests(sim.all_values()) for sim in sims]
     same = all(np.array_equal(d, digs[0]) and np.array_equal(sim.rounds(), rounds) for d, sim in zip(digs, sims))
+    same = same and np.array_equal(one_dig, digs[0]) and np.array_equal(one_rounds, rounds)
     dig = digs[0]
     for sim in sims:
         sim.close()
@@ -265,7 +323,8 @@ def leg_cfg3(ctx: Ctx, reps: int = 8) -> dict:
     parts.sort(key=lambda p: p[0])
     all_rounds = np.concatenate([np.frombuffer(p[1], dtype=np.uint32) for p in parts])
     all_dig = np.concatenate([np.frombuffer(p[2], dtype=np.uint8) for p in parts])
-    node_rounds = int(cfg.n_nodes) * int(all_rounds.astype(np.int64).sum()) * reps
+    node_rounds_one = int(cfg.n_nodes) * int(all_rounds.astype(np.int64).sum())
+    node_rounds = node_rounds_one * reps
     g = golden().get("cfg3", {})
     digest = combine_digests(all_dig)
     kmax = max(p[3] for p in parts) / 1e3
@@ -294,6 +353,9 @@ def leg_cfg3(ctx: Ctx, reps: int = 8) -> dict:
                         f"(SURVEY §A.10), sharded by global instance blocks; the batch run {reps} times "
                         f"back to back (one handle each) inside the timed region",
             "value": node_rounds / t_local, "unit": "node-rounds/s", "seconds": dt,
+            "single": {"what": "one run() of the batch on a fresh handle (no kernel events): the job's "
+                               "unamortised makespan, from the start barrier to the slowest rank's return",
+                       "value": node_rounds_one / t_one, "seconds": t_one},
             "seconds_before_closing_barrier": t_local, "value_through_closing_barrier": node_rounds / dt,
             "reps": reps,
             "node_rounds": node_rounds, "rounds_max": int(all_rounds.max()),
@@ -307,24 +369,45 @@ def leg_cfg3(ctx: Ctx, reps: int = 8) -> dict:
                             hashlib.sha256(all_rounds.astype("<u4").tobytes()).hexdigest() == g.get("rounds_sha256")}
 
 
-def leg_cfg5(ctx: Ctx, warm: int = 2, timed: int = 8) -> dict:
-    """BASELINE configs[4]: node partition over RCCL: the chunked send / receive exchange
-    overlapping phase B and the next round's phase A, or the per-round all-gather."""
+def _cfg5_handle(ctx: Ctx, cfg, xchunks):
+    """One cfg5 handle: the plain one-GPU handle at N = 1, else this rank's node partition over a
+    fresh RCCL communicator, with ACSIM_XCHUNKS set to `xchunks` while it is created (None: the
+    library's default sequence, the per-round all-gather for real ranks)."""
+    import acsim
+    if ctx.world == 1:
+        return acsim.Simulator(cfg, device=ctx.dev)
+    from acsim.distributed import partitioned_simulator
+    old = os.environ.get("ACSIM_XCHUNKS")
+    if xchunks is None:
+        os.environ.pop("ACSIM_XCHUNKS", None)
+    else:
+        os.environ["ACSIM_XCHUNKS"] = str(xchunks)
+    try:
+        return partitioned_simulator(cfg, ctx.rank, ctx.world, ctx.dev, group=ctx.group)
+    finally:
+        if old is None:
+            os.environ.pop("ACSIM_XCHUNKS", None)
+        else:
+            os.environ["ACSIM_XCHUNKS"] = old
+
+
+def _cfg5_sub(ctx: Ctx, warm: int, timed: int, xchunks) -> dict:
+    """Time one cfg5 exchange sequence on its own handle: `warm` + `timed` FIXED rounds, ms/round,
+    the exchange share (the part of a round outside the rank's own round kernels) and sha256(x^10)
+    against the golden hash."""
     import acsim
     from acsim.digest import sha256_values
     cfg = acsim.preset("cfg5", max_rounds=warm + timed)
     sim = None
     err = None
     try:
-        if ctx.world == 1:
-            sim = acsim.Simulator(cfg, device=ctx.dev)
-        else:
-            from acsim.distributed import partitioned_simulator
-            sim = partitioned_simulator(cfg, ctx.rank, ctx.world, ctx.dev, group=ctx.group)
+        sim = _cfg5_handle(ctx, cfg, xchunks)
     except Exception as e:  # noqa: BLE001
         err = f"{type(e).__name__}: {e}"
     if not ctx.all_ok(err is None):
-        raise RuntimeError(err or "another rank failed to create its cfg5 partition")
+        if sim is not None:
+            sim.close()
+        return {"error": err or "another rank failed to create its cfg5 partition"}
     kname = sim.kernel_name()
     sim.round(warm)
     sim.set_kernel_timing(True)
@@ -342,18 +425,43 @@ def leg_cfg5(ctx: Ctx, warm: int = 2, timed: int = 8) -> dict:
         h = sha256_values(x)
         g = golden().get("cfg5", {})
         n = int(cfg.n_nodes)
-        out = {"workload": f"cfg5: N=2^26 random 16-regular, trimmed t=5, FIXED; {warm} warm-up + "
-                           f"{timed} timed rounds, node-partitioned over {ctx.world} rank(s)"
-                           + ((" with the chunked RCCL exchange" if "xchunks" in kname
-                               else " with a per-round RCCL all-gather") if ctx.world > 1 else ""),
-               "value": n * timed / dt, "unit": "node-rounds/s", "ms_per_round": dt / timed * 1e3,
+        out = {"value": n * timed / dt, "unit": "node-rounds/s", "ms_per_round": dt / timed * 1e3,
                "kernel": kname, "round_kernel_ms_per_round": k_ms / max(1, k_n),
                "exchange_share": max(0.0, 1.0 - (k_ms / max(1, k_n)) / (dt / timed * 1e3)) if ctx.world > 1 else 0.0,
                "hbm_frac_unit": CFG5_BYTES_PER_NODE_ROUND * n * timed / dt / 1e9 / (HBM_PEAK_GBS * ctx.world),
-               "traffic": load_pmc_cfg5() if ctx.world == 1 else None,
                "rounds": rounds, "x_sha256": h,
-               "golden_match": rounds == 10 and h == g.get("x10_sha256")}
+               "golden_match": rounds == warm + timed and h == g.get("x10_sha256")}
     sim.close()
+    return out
+
+
+def leg_cfg5(ctx: Ctx, warm: int = 2, timed: int = 8) -> dict:
+    """BASELINE configs[4]: node partition over RCCL.  N = 1: one plain handle.  N > 1:
+    BOTH exchange sequences, each on its own handle and golden-checked: the default
+    per-round in-place all-gather, and the chunked grouped send / receive overlapping phase B and
+    the next round's phase A (ACSIM_XCHUNKS=4).  The leg's headline fields are the default
+    sequence's; `sequences` holds both."""
+    if ctx.world == 1:
+        out = _cfg5_sub(ctx, warm, timed, None)
+        if ctx.rank == 0 and "error" not in out:
+            out["workload"] = (f"cfg5: N=2^26 random 16-regular, trimmed t=5, FIXED; {warm} warm-up + {timed} "
+                               f"timed rounds on one GPU (two-level binned exchange)")
+            out["traffic"] = load_pmc_cfg5()
+        return out
+    seqs = {}
+    for name, xc in (("allgather", None), ("chunked", 4)):
+        try:
+            seqs[name] = _cfg5_sub(ctx, warm, timed, xc)
+        except Exception as e:  # noqa: BLE001
+            seqs[name] = {"error": f"{type(e).__name__}: {e}"}
+    if ctx.rank != 0:
+        return {}
+    out = dict(seqs["allgather"])
+    out["workload"] = (f"cfg5: N=2^26 random 16-regular, trimmed t=5, FIXED; {warm} warm-up + {timed} timed "
+                       f"rounds, node-partitioned over {ctx.world} ranks; headline fields: the per-round RCCL "
+                       f"all-gather (default); `sequences` also times the chunked send / receive exchange")
+    out["traffic"] = None
+    out["sequences"] = seqs
     return out
 
 

@@ -215,6 +215,11 @@ int acs_get_neighbors(struct acs_sim* sim, uint32_t* out, uint64_t n);
  * enable > 1 (each event pair idles the stream for a few µs, so the bench samples); enable < 0
  * brackets runs of -enable consecutive rounds with one pair each (a run ends at the end of an
  * acs_round / acs_run call at the latest) and counts every round of a run as one launch; 0 disables.
+ * A run's pair brackets EVERYTHING the handle enqueues between its first and last round, not only
+ * the round kernels: on node-partitioned handles the RCCL exchange, the (-min, max) all-reduce and
+ * the finalize; on EPS runs of long rounds, which wait for each 16-round chunk's verdict before
+ * enqueuing the next, the host round trip at a chunk boundary inside the run.  Use enable >= 1
+ * for a kernel-only figure there (bench.py uses run mode on the one-instance cfg4 legs only).
  * acs_get_kernel_timing returns the summed device time and bracketed launch count since the
  * last reset, plus the name of the round kernel in use. */
 int acs_set_kernel_timing(struct acs_sim* sim, int enable);

@@ -123,3 +123,27 @@ def test_rendezvous_single_rank_is_local():
     assert g.all_gather(5) == [5] and g.max(2.0) == 2.0 and g.broadcast(b"x") == b"x"
     g.barrier()
     g.close()
+
+
+def test_rendezvous_on_a_loopback_address_other_than_127_0_0_1():
+    """MASTER_ADDR = 127.0.1.1 (Debian's hostname mapping) or 127.0.0.2: rank 0 listens on the
+    address the other ranks connect to (it used to bind 127.0.0.1 for every 127.x
+    address, and the other rank was refused until the rendezvous timed out)."""
+    import threading
+    from acsim import rendezvous as R
+
+    for addr in ("127.0.0.2", "127.0.1.1"):
+        port, res = free_port(), {}
+
+        def serve():
+            g = R.Group(0, 2, addr, port, timeout=20.0, token="t")
+            res["gather"] = g.all_gather(0)
+            g.close()
+
+        t = threading.Thread(target=serve)
+        t.start()
+        g = R.Group(1, 2, addr, port, timeout=20.0, token="t")
+        mine = g.all_gather(1)
+        g.close()
+        t.join(30)
+        assert mine == [0, 1] and res["gather"] == [0, 1], addr

@@ -159,6 +159,39 @@ def test_cfg5_full_size_matches_golden():
     assert np.all(np.diff(tr) <= 0)
 
 
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_cfg5_write_through_stage_above_2gib(dtype):
+    """Write-through (sc1) phase-A stage stores (ACSIM_BIN_POL bit 64) on cfg5's two-level plan,
+    whose stage1 (2^30 deliveries: 8 GiB fp64, 4 GiB fp32) spans several re-based buffer
+    descriptors: every window's last pair must land (with 2 GiB windows it was
+    dropped by the range check).  fp64: x^3 against the oracle's golden hash; fp32: against the
+    default (nontemporal) stores of the same plan, bit for bit."""
+    g = GOLDEN["cfg5"]
+    over = {} if dtype == "f64" else {"dtype": "f32"}
+    pol = 4 | 32 | 1024 | 64 | 128   # the default switches with write-through phase-A stores
+    got = {}
+    for p in ((None, pol) if dtype == "f32" else (pol,)):
+        old = os.environ.get("ACSIM_BIN_POL")
+        if p is None:
+            os.environ.pop("ACSIM_BIN_POL", None)
+        else:
+            os.environ["ACSIM_BIN_POL"] = str(p)
+        try:
+            with acsim.Simulator(preset("cfg5", max_rounds=3, **over), device=0) as s:
+                assert s.kernel_name().startswith("k_bin_scatter+k_bin_regroup"), s.kernel_name()
+                s.run()
+                got[p] = sha256_values(s.values(0))
+        finally:
+            if old is None:
+                os.environ.pop("ACSIM_BIN_POL", None)
+            else:
+                os.environ["ACSIM_BIN_POL"] = old
+    if dtype == "f64":
+        assert got[pol] == g["x3_sha256"]
+    else:
+        assert got[pol] == got[None]
+
+
 def test_cfg5_full_size_eight_virtual_partitions():
     """The 8-GPU data flow of cfg5 (rows split in 8 blocks, each partition reading only its own
     copy of x, an all-gather after every round) on one device at full size: every private copy
