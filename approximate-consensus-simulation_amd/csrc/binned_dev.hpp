@@ -324,7 +324,11 @@ __device__ __forceinline__ void bin_dma_runs_pf(uint2 dsc, uint32_t nxt, uint32_
     for (uint32_t k = r0; k < r1; ++k) {
         const uint32_t so = __builtin_amdgcn_readlane(dsc.x, k);
         const uint32_t pre = __builtin_amdgcn_readlane(dsc.y, k);
+#if defined(ACS_DIAG_B) && ACS_DIAG_B == 3   // diagnostic: phase B without its stage transfer
+        const uint32_t n16 = (__builtin_amdgcn_readlane(nxt, k) - pre) / EPU > 0u ? 1u : 0u;
+#else
         const uint32_t n16 = (__builtin_amdgcn_readlane(nxt, k) - pre) / EPU;
+#endif
         const uint4* sp = s16 + so / EPU + lane;
         uint4* dp = d16 + (pre - base) / EPU;
         for (uint32_t o = 0; o < n16; o += 64)

@@ -36,6 +36,12 @@
 #include <mutex>
 #include <vector>
 
+// ACS_DIAG_B (variant builds only, tools/build_variant.sh; wrong values): the clean two-pass phase B
+// without 1 its selection network, 2 its position-dependent pick-up, 3 its stage DMA
+#ifndef ACS_DIAG_B
+#define ACS_DIAG_B 0
+#endif
+
 #include "binned_dev.hpp"
 
 namespace acs {
@@ -398,8 +404,13 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
         asm volatile("" : "+s"(sh0));
 #pragma unroll
         for (int t = 0; t < D; ++t) {
+#if ACS_DIAG_B == 2   // diagnostic: conflict-free reads that ignore the positions (kept live)
+            asm volatile("" ::"v"(pos_of(t)));
+            v[1 + t] = raw[(t * kBinSB + threadIdx.x) % cap];
+#else
             const uint32_t q = pos_of(t) + sh0;
             v[1 + t] = raw[q < cap ? q : cap];
+#endif
         }
         __syncthreads();   // every lane has read part 0 before part 1 overwrites the buffer's front
         bin_dma_runs_pf(pdsc, pnxt, nrun / NP + w * (nrun - nrun / NP) / NW, nrun / NP + (w + 1) * (nrun - nrun / NP) / NW,
@@ -407,8 +418,12 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
         __syncthreads();
 #pragma unroll
         for (int t = 0; t < D; ++t) {
+#if ACS_DIAG_B == 2
+            const VT u = raw[(t * kBinSB + threadIdx.x + 7) % cap];
+#else
             const uint32_t q = pos_of(t) - lo1;   // wraps above cap below lo1
             const VT u = raw[q < cap ? q : cap];
+#endif
             using UB = std::conditional_t<sizeof(VT) == 8, uint64_t, uint32_t>;
             v[1 + t] = __builtin_bit_cast(VT, (UB)(__builtin_bit_cast(UB, v[1 + t]) | __builtin_bit_cast(UB, u)));
         }
@@ -534,6 +549,10 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
             }
             if (VAR || (FAULTY && a.mp.omit))
                 res = apply_rule_reg_omit<D, T, WMSR>(a.rule, v, nmiss);
+#if ACS_DIAG_B == 1   // diagnostic: the plain sum instead of the selection network (wrong values)
+            else if (NP == 2 && !FLT)
+                res = tree_sum_const<D + 1>(v) / (VT)(D + 1);
+#endif
             else
                 res = apply_rule_reg<D, T, WMSR>(a.rule, v);
         }
