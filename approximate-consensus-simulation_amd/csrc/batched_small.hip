@@ -413,7 +413,8 @@ __global__ __launch_bounds__(64 * F, (F == 2 && sizeof(VT) == 8 && ACS_SPLIT_WPE
 uint32_t batched_split_factor(uint32_t N, uint32_t rule, bool faults) {
     if (N != 64 || rule != 0 || faults) return 1;
     // default 2: at 10^5 instances as fast as one lane per receiver (2.08 ms either way), and the
-    // 8-rank shard's tail shrinks (0.300 -> 0.281 ms); 4 costs 26 % more work (profiles/r03_s02_cfg3_split.jsonl)
+    // 8-rank shard's tail shrinks (0.300 -> 0.281 ms); 4 costs about 25 % more work (re-measured in
+    // round 5 beside the default: profiles/r05_cfg3_split_factor.jsonl, tools/cfg3_shard_probe.py)
     uint32_t F = 2;
     if (const char* v = getenv("ACSIM_BATCH_SPLIT")) F = (uint32_t)strtoul(v, nullptr, 10);
     return F == 2 || F == 4 ? F : 1;

@@ -24,6 +24,10 @@ constexpr uint32_t kPolNtStoreM = 128;  // phase M (two-level plans): nontempora
 constexpr uint32_t kPolSc1StoreM = 256; // phase M: write-through (sc1) stage-2 stores
 constexpr uint32_t kPolSc1X = 512;      // phase B: write-through (sc1) stores of x^{r+1}
 constexpr uint32_t kPolClampPick = 1024; // phase B (NP = 2): pick-up by clamped index into a zero slot, OR-merged
+// (2048: a scalar-descriptor buffer LDS-DMA form of phase B's run copies, measured slower in round 5
+// and removed)
+constexpr uint32_t kPolBytePick = 4096;  // phase B (clamped pick-up, clean plans): packed 16-bit pick-up, add-merged
+constexpr uint32_t kPolMask = 8191;      // every switch (ACSIM_BIN_POL)
 // Default switches (the stage-store bits are chosen per plan).  Until round 4 the
 // stream's store flavour was a runtime argument, and the compiler merged the nontemporal and the
 // plain store of its two branches into one plain store: every "nontemporal stage store" measured
@@ -35,8 +39,9 @@ constexpr uint32_t kPolClampPick = 1024; // phase B (NP = 2): pick-up by clamped
 // 7.60 against 7.86 ms per round for plain ones (the 16 GiB of stages far exceed the MALL)
 constexpr uint32_t kPolOneLevelStores = kPolSc1Store;
 constexpr uint32_t kPolTwoLevelStores = kPolNtStore | kPolNtStoreM;
-constexpr uint32_t kPolDefault = kPolNtInv | kPolBfPick | kPolClampPick;   // measured (cfg4): phase B 80 -> 71 (nt
-// invpos) -> 63.2 us (pick-up); the clamped pick-up: round 117.2-118.8 -> 112.3-112.9 us
+constexpr uint32_t kPolDefault = kPolNtInv | kPolBfPick | kPolClampPick | kPolBytePick;   // measured (cfg4): phase B
+// 80 -> 71 (nt invpos) -> 63.2 us (pick-up); the clamped pick-up: round 117.2-118.8 -> 112.3-112.9 us (DESIGN.md
+// §5.10); the packed 16-bit pick-up: 112.2-113.0 -> 110.2-111.0 us (§5.11)
 
 // ------------------------------------------------------------------------------ shared pieces
 // Stream [p0, p1) of an index stream: out[p] = lds[idx[p]].  Super-steps of 512 positions per

@@ -191,8 +191,8 @@ struct BinnedPlan {
     double* stage1 = nullptr;           // [Ep1]
     double* stage2 = nullptr;           // [Ep2] (two levels)
     double* xtag = nullptr;             // [N+2] tagged sender values (fault schedules only)
-    uint64_t* ts = nullptr;             // ACSIM_BIN_TS=<file>: [3 * (ts_a + ts_b)] workgroup timestamps of the last round
-    uint32_t ts_a = 0, ts_b = 0;        // phase-A / phase-B workgroups recorded
+    uint64_t* ts = nullptr;             // ACSIM_BIN_TS=<file>: [3 * (ts_a + ts_b + ts_m)] workgroup timestamps of the last round
+    uint32_t ts_a = 0, ts_b = 0, ts_m = 0;   // phase-A / phase-B / phase-M workgroups recorded
     // fault fix-up: fix[k] = (last-stage position, local row, slot, sender) of every
     // delivery from a sender that is not honest; nullptr: tagged senders (k_bin_tag) instead
     uint4* fix = nullptr;

@@ -170,16 +170,19 @@ template <typename VT = double>
 __global__ __launch_bounds__(kBinA) void k_bin_regroup(const VT* __restrict__ stage1, const uint2* __restrict__ mt,
                                                      const uint64_t* __restrict__ moff, const uint16_t* __restrict__ idxM,
                                                      VT* __restrict__ stage2, const InstState* __restrict__ st,
-                                                     uint32_t PK, uint32_t pol) {
+                                                     uint32_t PK, uint32_t pol, uint64_t* __restrict__ ts) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lm_raw[];
     VT* lm = reinterpret_cast<VT*>(lm_raw);
     if (st->done) return;
+    const uint64_t t0 = ts ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint32_t g = blockIdx.x;
     constexpr uint32_t NW = kBinA / 64;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     bin_dma_runs(mt + (uint64_t)g * (PK + 1), w * PK / NW, (w + 1) * PK / NW, stage1, lm);
     __syncthreads();
+    const uint64_t t1 = ts ? __builtin_amdgcn_s_memrealtime() : 0;
     bin_stream(lm, idxM, stage2, moff[g], moff[g + 1], (pol & kPolSc1StoreM) ? 2u : (pol & kPolNtStoreM) ? 1u : 0u);
+    if (ts) bin_ts(ts, t0, t1);
 }
 
 // ------------------------------------------------------------------------------ phase B
@@ -393,6 +396,61 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
         if (a.ts) t1 = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
         for (int t = 0; t < D; ++t) v[1 + t] = raw[pos_of(t)];
+    } else if (sizeof(VT) == 8 && clampm && !FLT && (pol & kPolBytePick)) {
+        // Packed 16-bit pick-up (kPolBytePick, clean plans).  A u32 of invpos holds
+        // two slots' positions: one v_pk_add_u16 shifts both into the part's buffer frame, one
+        // v_pk_min_u16 clamps both to the zero slot at cap, and each becomes a byte offset by one
+        // shift (the low half by an SDWA shift of its WORD_0; the high half by >> 13, exact because
+        // both clamped halves are < cap < 2^13, so the low half's bits 13-15 are zero).  Part 1's
+        // value is merged by one fp64 add: +0.0 is the identity for every value a clean round
+        // carries (finite, never -0.0).  2 VALU per slot and part + 1 per slot for the merge,
+        // against 3 + 3 + 2.  Positions p + (cap - hi0) stay below 2^16 (p < 2^14, cap < 2^13), and
+        // p - lo1 for a part-0 slot wraps to at least 2^16 - 2^14 > cap.
+        static_assert(cap < 8192, "two clamped positions per u32: each below 2^13");
+        using us2 = unsigned short __attribute__((ext_vector_type(2)));
+        const us2 cap2 = {(unsigned short)cap, (unsigned short)cap};
+        const unsigned char* rb = reinterpret_cast<const unsigned char*>(raw);
+        auto pick = [&](uint32_t word, const us2 sh, bool sub, VT& lo, VT& hi) {
+            us2 q = __builtin_bit_cast(us2, word);
+            q = sub ? q - sh : q + sh;
+            q = __builtin_elementwise_min(q, cap2);
+            const uint32_t qw = __builtin_bit_cast(uint32_t, q);
+            uint32_t blo;
+            asm("v_lshlrev_b32_sdwa %0, 3, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
+                : "=v"(blo) : "v"(qw));
+            lo = *reinterpret_cast<const VT*>(rb + blo);
+            hi = *reinterpret_cast<const VT*>(rb + (qw >> 13));
+        };
+        __syncthreads();
+        if (a.ts) t1 = __builtin_amdgcn_s_memrealtime();
+        uint32_t sh0 = cap - hi0;
+        asm volatile("" : "+s"(sh0));   // (opaque: see the clamped branch below)
+        const us2 s0 = {(unsigned short)sh0, (unsigned short)sh0};
+#pragma unroll
+        for (int q = 0; q < D / 8; ++q) {
+            pick(ip[q].x, s0, false, v[1 + 8 * q], v[2 + 8 * q]);
+            pick(ip[q].y, s0, false, v[3 + 8 * q], v[4 + 8 * q]);
+            pick(ip[q].z, s0, false, v[5 + 8 * q], v[6 + 8 * q]);
+            pick(ip[q].w, s0, false, v[7 + 8 * q], v[8 + 8 * q]);
+        }
+        __syncthreads();   // every lane has read part 0 before part 1 overwrites the buffer's front
+        const uint32_t lo1 = hi0, j1 = nrun / NP;
+        bin_dma_runs_pf(pdsc, pnxt, j1 + w * (nrun - j1) / NW, j1 + (w + 1) * (nrun - j1) / NW, stage, raw, lo1);
+        __syncthreads();
+        uint32_t l1 = lo1;
+        asm volatile("" : "+s"(l1));
+        const us2 s1 = {(unsigned short)l1, (unsigned short)l1};
+#pragma unroll
+        for (int q = 0; q < D / 8; ++q) {
+            const uint32_t wd[4] = {ip[q].x, ip[q].y, ip[q].z, ip[q].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                VT u0, u1;
+                pick(wd[e], s1, true, u0, u1);
+                v[1 + 8 * q + 2 * e] = v[1 + 8 * q + 2 * e] + u0;
+                v[2 + 8 * q + 2 * e] = v[2 + 8 * q + 2 * e] + u1;
+            }
+        }
     } else if (sizeof(VT) == 8 && clampm) {
         const uint32_t lo1 = hi0;
         // part 0
@@ -553,6 +611,8 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
             else if (NP == 2 && !FLT)
                 res = tree_sum_const<D + 1>(v) / (VT)(D + 1);
 #endif
+            else if constexpr (!FLT)   // padding adds skipped, exact for every input (sortnet.hpp)
+                res = apply_rule_reg<D, T, WMSR, true>(a.rule, v);
             else
                 res = apply_rule_reg<D, T, WMSR>(a.rule, v);
         }
@@ -1005,13 +1065,14 @@ uint32_t binned_levels(uint64_t N, uint64_t NR, uint32_t d, uint32_t sa, uint32_
 
 void binned_free(BinnedPlan& p) {
     if (p.ts) {   // diagnostic dump: phase,workgroup,t_entry,t_staged,t_end (100 MHz ticks)
-        std::vector<uint64_t> h(3ull * (p.ts_a + p.ts_b));
+        std::vector<uint64_t> h(3ull * (p.ts_a + p.ts_b + p.ts_m));
         const char* fn = getenv("ACSIM_BIN_TS");
         if (fn && hipMemcpy(h.data(), p.ts, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
             if (FILE* f = fopen(fn, "w")) {
-                for (uint64_t k = 0; k < p.ts_a + p.ts_b; ++k)
-                    fprintf(f, "%c,%llu,%llu,%llu,%llu\n", k < p.ts_a ? 'A' : 'B',
-                            (unsigned long long)(k < p.ts_a ? k : k - p.ts_a), (unsigned long long)h[3 * k],
+                for (uint64_t k = 0; k < p.ts_a + p.ts_b + p.ts_m; ++k)
+                    fprintf(f, "%c,%llu,%llu,%llu,%llu\n", k < p.ts_a ? 'A' : k < p.ts_a + p.ts_b ? 'B' : 'M',
+                            (unsigned long long)(k < p.ts_a ? k : k < p.ts_a + p.ts_b ? k - p.ts_a : k - p.ts_a - p.ts_b),
+                            (unsigned long long)h[3 * k],
                             (unsigned long long)h[3 * k + 1], (unsigned long long)h[3 * k + 2]);
                 fclose(f);
             }
@@ -1237,7 +1298,8 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     p.ofree = ofree;
     {
         const char* v = getenv("ACSIM_BIN_POL");
-        p.pol = v ? (uint32_t)strtoul(v, nullptr, 0) & 2047u : kPolDefault | (G.levels == 2 ? kPolTwoLevelStores : kPolOneLevelStores);
+        p.pol = v ? (uint32_t)strtoul(v, nullptr, 0) & kPolMask
+                  : kPolDefault | (G.levels == 2 ? kPolTwoLevelStores : kPolOneLevelStores);
     }
     if (ofree) {   // order-free phase B: receiver ids in image order
         p.rstride = ((uint32_t)d * kBinSB + p.nrun * (G.pad - 1) + 15u) & ~15u;
@@ -1344,8 +1406,9 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     if (e == hipSuccess && getenv("ACSIM_BIN_TS")) {   // diagnostic workgroup timestamps
         p.ts_a = (p.P + 7) / 8 * 8 * p.segs;
         p.ts_b = (p.Q + 7) / 8 * 8;
-        e = hipMalloc(&p.ts, 3ull * (p.ts_a + p.ts_b) * sizeof(uint64_t));
-        if (e == hipSuccess) e = hipMemset(p.ts, 0, 3ull * (p.ts_a + p.ts_b) * sizeof(uint64_t));
+        p.ts_m = p.ngroups;
+        e = hipMalloc(&p.ts, 3ull * (p.ts_a + p.ts_b + p.ts_m) * sizeof(uint64_t));
+        if (e == hipSuccess) e = hipMemset(p.ts, 0, 3ull * (p.ts_a + p.ts_b + p.ts_m) * sizeof(uint64_t));
     }
     T1.release();
     T2.release();
@@ -1429,7 +1492,8 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
             float* st2 = reinterpret_cast<float*>(p.stage2);
             if (phases & 2)
                 hipLaunchKernelGGL(k_bin_regroup<float>, dim3(p.ngroups), dim3(kBinA), (p.mcap + 4) * sizeof(float), s, st1,
-                                   p.mt, p.moff, p.idxM, st2, a.st, p.PK, pol);
+                                   p.mt, p.moff, p.idxM, st2, a.st, p.PK, pol,
+                                   p.ts ? p.ts + 3ull * (p.ts_a + p.ts_b) : nullptr);
             st1 = st2;   // phase B reads the regrouped stage
         }
         if (fixp)
@@ -1491,7 +1555,8 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
     if (p.levels == 2) {
         if (phases & 2)
             hipLaunchKernelGGL(k_bin_regroup<double>, dim3(p.ngroups), dim3(kBinA), (p.mcap + 2) * sizeof(double), s,
-                               p.stage1, p.mt, p.moff, p.idxM, p.stage2, a.st, p.PK, pol);
+                               p.stage1, p.mt, p.moff, p.idxM, p.stage2, a.st, p.PK, pol,
+                               p.ts ? p.ts + 3ull * (p.ts_a + p.ts_b) : nullptr);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         last = p.stage2;
     }

@@ -42,15 +42,15 @@ __device__ __forceinline__ VT wmsr_reg(VT (&v)[D + 1], uint32_t nmiss = 0) {
 }
 
 // WMSR = true instantiates the W-MSR rule only (a separate kernel instantiation, so the other
-// rules' kernels carry none of its registers).
-template <int D, int T, bool WMSR = false, typename VT>
+// rules' kernels carry none of its registers).  NZ: no value is -0.0 (tree_sum_const).
+template <int D, int T, bool WMSR = false, bool NZ = false, typename VT>
 __device__ __forceinline__ VT apply_rule_reg(uint32_t rule, VT (&v)[D + 1]) {
     constexpr int M = D + 1;
     if constexpr (WMSR) {
         return wmsr_reg<D, T>(v);
     }
     if constexpr (T == 0) {
-        if (rule == 0) return tree_sum_const<M>(v) / (VT)M;       // AVERAGE: entry order
+        if (rule == 0) return tree_sum_const<M, 0, 1, NZ>(v) / (VT)M;       // AVERAGE: entry order
     }
     select_sort<M, T, M - T>(v);
     constexpr int NR = M - 2 * T;
@@ -58,10 +58,10 @@ __device__ __forceinline__ VT apply_rule_reg(uint32_t rule, VT (&v)[D + 1]) {
     if constexpr (T >= 1) {
         if (rule == 3) {                                             // DLPSW: R[0], R[T], ...
             constexpr int NQ = (NR + T - 1) / T;
-            return tree_sum_const<NQ, T, T>(v) / (VT)NQ;
+            return tree_sum_const<NQ, T, T, NZ>(v) / (VT)NQ;
         }
     }
-    return tree_sum_const<NR, T>(v) / (VT)NR;                        // TRIMMED_MEAN
+    return tree_sum_const<NR, T, 1, NZ>(v) / (VT)NR;                        // TRIMMED_MEAN
 }
 
 // The rules over a receiver with nmiss absent entries (DESIGN.md §9 missing_policy = OMIT; CSR

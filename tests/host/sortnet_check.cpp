@@ -1,0 +1,69 @@
+// Host check of csrc/sortnet.hpp (compiled with g++ by tests/test_sortnet_host.py):
+//  1. every selection network the register kernels instantiate (M = d + 1 entries, window [t, M - t))
+//     puts the window's order statistics where std::sort does, on random multisets with ties;
+//  2. the NZ tree sum (padding adds skipped, one final +0.0) equals the spec's tree bit for bit,
+//     signed zeros and denormals included.
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <random>
+
+#define __device__
+#define __forceinline__ inline
+#include "sortnet.hpp"
+
+using namespace acs;
+
+static uint64_t bits(double x) {
+    uint64_t u;
+    memcpy(&u, &x, 8);
+    return u;
+}
+
+template <int M, int LO, int HI>
+static long check_net(std::mt19937_64& g, int iters) {
+    long bad = 0;
+    for (int it = 0; it < iters; ++it) {
+        double v[M], ref[M];
+        for (int k = 0; k < M; ++k) v[k] = ref[k] = (double)(int)(g() % 9) * 0.125 + (g() % 4 ? 0.0 : 1e-3 * (g() % 7));
+        select_sort<M, LO, HI>(v);
+        std::sort(ref, ref + M);
+        for (int k = LO; k < HI; ++k) bad += bits(v[k]) != bits(ref[k]);
+    }
+    return bad;
+}
+
+template <int N, int OFF, int STRIDE, int M>
+static long check_tree(const double (&a)[M]) {
+    return bits(tree_sum_const<N, OFF, STRIDE, false>(a)) != bits(tree_sum_const<N, OFF, STRIDE, true>(a));
+}
+
+int main() {
+    std::mt19937_64 g(7);
+    long bad = 0;
+    bad += check_net<33, 5, 28>(g, 200000);   // cfg4: d = 32, t = 5
+    bad += check_net<33, 0, 33>(g, 100000);   // d = 32, t = 0 (full sort)
+    bad += check_net<17, 5, 12>(g, 200000);   // cfg5: d = 16, t = 5
+    bad += check_net<17, 0, 17>(g, 100000);
+    bad += check_net<9, 2, 7>(g, 100000);     // d = 8, t = 2
+    bad += check_net<5, 1, 4>(g, 100000);     // d = 4, t = 1
+    long nbad_net = bad;
+    const double pool[] = {0.0, -0.0, 5e-324, -5e-324, 1.0, -1.0, 0.5, -0.5, 1e-310, -1e-310, 3.0, -3.0};
+    long ntree = 0;
+    for (int it = 0; it < 300000; ++it) {
+        double a[33];
+        for (int k = 0; k < 33; ++k) {
+            const int c = (int)(g() % 14);
+            a[k] = c < 12 ? pool[c] : (double)((int64_t)(g() % 2001) - 1000) * 0.25;
+        }
+        bad += check_tree<23, 5, 1>(a);    // TRIMMED t = 5 of 33
+        bad += check_tree<5, 5, 5>(a);     // DLPSW t = 5
+        bad += check_tree<33, 0, 1>(a);    // AVERAGE over 33 entries
+        bad += check_tree<7, 5, 1>(a);     // TRIMMED t = 5 of 17
+        bad += check_tree<16, 0, 1>(a);    // a power of two: nothing skipped
+        ntree += 5;
+    }
+    printf("networks: %ld mismatches; trees: %ld checked, %ld mismatches\n", nbad_net, ntree, bad - nbad_net);
+    return bad != 0;
+}

@@ -294,6 +294,11 @@ def test_cache_policy_switches_bit_exact(oracle_mod, name, pol):
 
 @pytest.mark.parametrize("name,pol,pack", [
     ("d32_t5_eps_n50000_sa1024", 1124, 1), ("d32_t5_eps_n50000_sa1024", 1060, 1),
+    # the packed 16-bit pick-up (4096, the default since round 5); the faulty plan
+    # keeps the OR-merged pick-up with the switch set
+    ("d32_t5_eps_n50000_sa1024", 1124 | 4096, 1), ("d32_t5_dlpsw_sa2048", 1124 | 4096, 1),
+    ("cfg4_shape_2e17", 1124 | 4096, 1), ("d32_avg_clean_sa1024", 1124 | 4096, 1),
+    ("faulty_d32_t5_byzrandom_drop_sa1024", 1124 | 4096, 1), ("d32_t5_eps_n50000_sa1024", 1124 | 4096, 0),
     ("d32_t5_dlpsw_sa2048", 1124, 1), ("cfg4_shape_2e17", 1124, 1),
     ("faulty_d32_t5_byzrandom_drop_sa1024", 1124, 1), ("d32_avg_clean_sa1024", 1124, 1)])
 def test_clamped_pickup_bit_exact(oracle_mod, name, pol, pack):

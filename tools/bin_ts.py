@@ -6,7 +6,7 @@ import sys
 import numpy as np
 
 rows = [ln.strip().split(",") for ln in open(sys.argv[1]) if ln.strip()]
-for ph in ("A", "B"):
+for ph in ("A", "M", "B"):
     t = np.array([[int(v) for v in r[2:5]] for r in rows if r[0] == ph and int(r[2]) > 0], dtype=np.int64)
     if not len(t):
         continue
