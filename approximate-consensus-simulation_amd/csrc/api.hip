@@ -789,6 +789,10 @@ static int advance(acs_sim* s, uint32_t k) {
         return ACS_OK;
     }
     const bool eps_mode = s->c.termination == ACS_TERM_EPS;
+    // FIXED runs need no verdict between chunks: the deferred finalize of a chunk's last round is
+    // folded by the next chunk's first phase A like any other, and one standalone finalize closes
+    // the call (round 5: one 4.7 µs k_finalize per 16 rounds fewer)
+    const bool chunk_flush = eps_mode || s->partitioned;
     // Long rounds (a chunk of them takes milliseconds): wait for each chunk's verdict before
     // enqueuing the next, so no chunk of no-op launches follows convergence (the host wake-up is
     // < 1 % of a chunk).  Short rounds keep one chunk in flight and poll the previous one.
@@ -802,7 +806,8 @@ static int advance(acs_sim* s, uint32_t k) {
             int rc = enqueue_round(s, s->round + q);
             if (rc) return rc;
         }
-        if (int rc = flush_finalize(s)) return rc;
+        if (chunk_flush)
+            if (int rc = flush_finalize(s)) return rc;
         if (s->xchunks) HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_fin, 0));   // verdicts land on cstream
         s->round += chunk;
         k -= chunk;
@@ -827,9 +832,14 @@ static int advance(acs_sim* s, uint32_t k) {
     }
     for (hipEvent_t e : poll)
         if (e) (void)hipEventDestroy(e);
-    if (s->run_end) {   // a timing run cut short by the end of this call
-        if (int rc = flush_finalize(s)) return rc;
+    if (int rc = flush_finalize(s)) return rc;   // (FIXED: the call's last round)
+    if (s->run_end)   // a timing run cut short by the end of this call
         if (int rc = timing_close(s)) return rc;
+    if (!eps_mode) {
+        // FIXED: every instance is done exactly at max_rounds, so no device round trip is needed
+        // here (acs_round's state read and acs_run's summary synchronise the stream anyway)
+        s->all_done = s->round >= s->c.max_rounds;
+        return ACS_OK;
     }
     HIP_TRY(hipMemcpyAsync(s->h_ndone, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
