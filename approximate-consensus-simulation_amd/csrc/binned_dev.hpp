@@ -27,7 +27,8 @@ constexpr uint32_t kPolClampPick = 1024; // phase B (NP = 2): pick-up by clamped
 // (2048: a scalar-descriptor buffer LDS-DMA form of phase B's run copies, measured slower in round 5
 // and removed)
 constexpr uint32_t kPolBytePick = 4096;  // phase B (clamped pick-up, clean plans): packed 16-bit pick-up, add-merged
-constexpr uint32_t kPolMask = 8191;      // every switch (ACSIM_BIN_POL)
+constexpr uint32_t kPolAsmDma = 8192;    // phase B (clamped pick-up): run copies by asm saddr LDS-DMA (bin_dma_runs_asm)
+constexpr uint32_t kPolMask = 16383;     // every switch (ACSIM_BIN_POL)
 // Default switches (the stage-store bits are chosen per plan).  Until round 4 the
 // stream's store flavour was a runtime argument, and the compiler merged the nontemporal and the
 // plain store of its two branches into one plain store: every "nontemporal stage store" measured
@@ -39,9 +40,10 @@ constexpr uint32_t kPolMask = 8191;      // every switch (ACSIM_BIN_POL)
 // 7.60 against 7.86 ms per round for plain ones (the 16 GiB of stages far exceed the MALL)
 constexpr uint32_t kPolOneLevelStores = kPolSc1Store;
 constexpr uint32_t kPolTwoLevelStores = kPolNtStore | kPolNtStoreM;
-constexpr uint32_t kPolDefault = kPolNtInv | kPolBfPick | kPolClampPick | kPolBytePick;   // measured (cfg4): phase B
-// 80 -> 71 (nt invpos) -> 63.2 us (pick-up); the clamped pick-up: round 117.2-118.8 -> 112.3-112.9 us (DESIGN.md
-// §5.10); the packed 16-bit pick-up: 112.2-113.0 -> 110.2-111.0 us (§5.11)
+constexpr uint32_t kPolDefault = kPolNtInv | kPolBfPick | kPolClampPick | kPolBytePick | kPolAsmDma;   // measured
+// (cfg4): phase B 80 -> 71 (nt invpos) -> 63.2 us (pick-up); the clamped pick-up: round 117.2-118.8 -> 112.3-112.9
+// us; the packed 16-bit pick-up: 112.2-113.0 -> 110.2-111.0 us; the asm run copies: a further
+// -0.4 us (§5.11)
 
 // ------------------------------------------------------------------------------ shared pieces
 // Stream [p0, p1) of an index stream: out[p] = lds[idx[p]].  Super-steps of 512 positions per
@@ -340,6 +342,34 @@ __device__ __forceinline__ void bin_dma_runs_pf(uint2 dsc, uint32_t nxt, uint32_
             if (o + lane < n16) __builtin_amdgcn_global_load_lds(sp + o, dp + o, 16, 0, 0);
     }
 }
+
+// bin_dma_runs_pf with the copies issued as asm `global_load_lds_dwordx4 voffset, sbase` (kPolAsmDma,
+// DESIGN.md §5.11): the run's stage address is an SGPR pair (stage + start, SALU) and the per-lane
+// offset the fixed lane * 16, and the LDS destination goes to M0 in the same statement, so a run
+// costs two readlanes (its start, and its image offset and length packed as pre | n16 << 16 by the
+// caller, one u32 per lane) and one tail compare per 64-unit column — against ≈ 9 VALU with the
+// compiler's 64-bit per-lane addresses.  The compiler does not count these loads: the caller waits
+// `vmcnt(0)` itself before the barrier that publishes the part (bin_dma_wait).
+template <typename VT = double>
+__device__ __forceinline__ void bin_dma_runs_asm(uint32_t so_l, uint32_t pk_l, uint32_t r0, uint32_t r1,
+                                                 const VT* __restrict__ src, VT* dst, uint32_t base) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t lane = threadIdx.x & 63, voff = lane * 16u;
+    const uint32_t lb = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)dst;
+    for (uint32_t k = r0; k < r1; ++k) {
+        const uint32_t so = __builtin_amdgcn_readlane(so_l, k), pq = __builtin_amdgcn_readlane(pk_l, k);
+        const uint32_t pre = pq & 0xFFFFu, n16 = pq >> 16;
+        // the start's low bits carry the run's pad count (round_binned.hip tiles): mask them off
+        const uint64_t sb = (uint64_t)(uintptr_t)src + (uint64_t)(so & ~(16u / sizeof(VT) - 1u)) * sizeof(VT);
+        const uint32_t m0 = lb + (pre - base) * (uint32_t)sizeof(VT);
+        for (uint32_t o = 0; o < n16; o += 64)
+            if (lane < n16 - o)
+                asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+                             :: "v"(voff), "s"(sb + o * 16u), "s"(m0 + o * 16u) : "memory");
+    }
+#endif
+}
+__device__ __forceinline__ void bin_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // diagnostic (ACSIM_BIN_TS): workgroup entry, end of its staging wait, end, in 100 MHz ticks
 __device__ __forceinline__ void bin_ts(uint64_t* ts, uint64_t t0, uint64_t t1) {

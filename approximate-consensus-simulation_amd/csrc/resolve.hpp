@@ -2,6 +2,7 @@
 #pragma once
 
 #include "engine.hpp"
+#include "sortnet.hpp"
 
 namespace acs {
 
@@ -57,6 +58,37 @@ __device__ __forceinline__ double wave_max(double v) {
     return v;
 }
 
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+    return __hiloint2double(hi, lo);
+}
+// Wave-wide fp64 min / max through DPP instead of ds_bpermute butterflies (round 5, DESIGN.md
+// §5.11): quad swaps, row rotations by 4 and 8, then row_bcast15 / row_bcast31 fold the four rows
+// into lane 63, which is read back wave-uniform.  No LDS round trips on the block's exit path,
+// 3 VALU per step.  Every lane must hold a non-NaN value (the callers pass +-inf for idle lanes).
+template <bool MAX, int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_minmax_step(double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(v), __double2loint(v), CTRL, ROW_MASK, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(v), __double2hiint(v), CTRL, ROW_MASK, 0xF, false);
+    const double u = __hiloint2double(hi, lo);
+    return MAX ? ce_max(v, u) : ce_min(v, u);
+#else
+    return v;
+#endif
+}
+template <bool MAX>
+__device__ __forceinline__ double wave_minmax_dpp(double v) {
+    v = dpp_minmax_step<MAX, 0xB1, 0xF>(v);    // quad_perm [1,0,3,2]
+    v = dpp_minmax_step<MAX, 0x4E, 0xF>(v);    // quad_perm [2,3,0,1]
+    v = dpp_minmax_step<MAX, 0x124, 0xF>(v);   // row_ror:4
+    v = dpp_minmax_step<MAX, 0x128, 0xF>(v);   // row_ror:8   (every lane: its row of 16)
+    v = dpp_minmax_step<MAX, 0x142, 0xA>(v);   // row_bcast:15 into rows 1, 3
+    v = dpp_minmax_step<MAX, 0x143, 0xC>(v);   // row_bcast:31 into rows 2, 3 (lane 63: all four rows)
+    return readlane_f64(v, 63);
+}
+
 // EPS verdict publication (RoundArgs::eacc): a double's bits mapped so that unsigned order is numeric
 // order (for non-NaN values), and back.  Block b folds into pair b % kEaccSlots (one 128-B line each,
 // so the blocks' device-scope atomics spread over 32 addresses instead of queueing on one); word 0
@@ -82,8 +114,8 @@ __device__ __forceinline__ void block_minmax_store(double mn, double mx, double2
                                                    unsigned long long* eacc = nullptr) {
     static_assert(BS % 64 == 0, "block must be whole wavefronts");
     constexpr int NW = BS / 64;
-    mn = wave_min(mn);
-    mx = wave_max(mx);
+    mn = wave_minmax_dpp<false>(mn);
+    mx = wave_minmax_dpp<true>(mx);
     if constexpr (NW == 1) {
         if (threadIdx.x == 0) {
             *out = make_double2(mn, mx);
@@ -107,11 +139,6 @@ __device__ __forceinline__ void block_minmax_store(double mn, double mx, double2
     }
 }
 
-__device__ __forceinline__ double readlane_f64(double v, int lane) {
-    const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
-    return __hiloint2double(hi, lo);
-}
 __device__ __forceinline__ double readlane_v(double v, int lane) { return readlane_f64(v, lane); }
 __device__ __forceinline__ float readlane_v(float v, int lane) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));

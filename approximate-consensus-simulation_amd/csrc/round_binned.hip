@@ -312,6 +312,8 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
     constexpr uint32_t cap = kBinPartCap<D, NP>;
     const bool clampm = NP == 2 && sizeof(VT) == 8 && !FAULTY && pf && (pol & kPolClampPick);
     uint32_t hi0 = 0;
+    const bool adma = clampm && (pol & kPolAsmDma);   // asm saddr LDS-DMA (binned_dev.hpp)
+    uint32_t ppk = 0;                                   // this lane's run: image offset | 16-B units << 16
     if (pf) {
         const uint32_t lane = threadIdx.x & 63;
         if (lane < nrun) {
@@ -320,7 +322,12 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
         }
         const uint32_t j1 = nrun / NP;
         hi0 = __builtin_amdgcn_readlane(pdsc.y, j1);
-        bin_dma_runs_pf(pdsc, pnxt, w * j1 / NW, (w + 1) * j1 / NW, stage, raw, clampm ? hi0 - cap : 0u);
+        if (adma) {
+            ppk = pdsc.y | ((pnxt - pdsc.y) / (16 / sizeof(VT))) << 16;
+            bin_dma_runs_asm(pdsc.x, ppk, w * j1 / NW, (w + 1) * j1 / NW, stage, raw, hi0 - cap);
+        } else {
+            bin_dma_runs_pf(pdsc, pnxt, w * j1 / NW, (w + 1) * j1 / NW, stage, raw, clampm ? hi0 - cap : 0u);
+        }
     }
     if constexpr (NP > 1) {
         if (clampm && threadIdx.x < 16 / sizeof(VT)) raw[cap + threadIdx.x] = VT(0);   // +0 bits
@@ -421,6 +428,7 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
             lo = *reinterpret_cast<const VT*>(rb + blo);
             hi = *reinterpret_cast<const VT*>(rb + (qw >> 13));
         };
+        if (adma) bin_dma_wait();   // (the asm copies are not in the compiler's count)
         __syncthreads();
         if (a.ts) t1 = __builtin_amdgcn_s_memrealtime();
         uint32_t sh0 = cap - hi0;
@@ -435,7 +443,12 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
         }
         __syncthreads();   // every lane has read part 0 before part 1 overwrites the buffer's front
         const uint32_t lo1 = hi0, j1 = nrun / NP;
-        bin_dma_runs_pf(pdsc, pnxt, j1 + w * (nrun - j1) / NW, j1 + (w + 1) * (nrun - j1) / NW, stage, raw, lo1);
+        if (adma) {
+            bin_dma_runs_asm(pdsc.x, ppk, j1 + w * (nrun - j1) / NW, j1 + (w + 1) * (nrun - j1) / NW, stage, raw, lo1);
+            bin_dma_wait();
+        } else {
+            bin_dma_runs_pf(pdsc, pnxt, j1 + w * (nrun - j1) / NW, j1 + (w + 1) * (nrun - j1) / NW, stage, raw, lo1);
+        }
         __syncthreads();
         uint32_t l1 = lo1;
         asm volatile("" : "+s"(l1));
@@ -454,6 +467,7 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
     } else if (sizeof(VT) == 8 && clampm) {
         const uint32_t lo1 = hi0;
         // part 0
+        if (adma) bin_dma_wait();
         __syncthreads();
         if (a.ts) t1 = __builtin_amdgcn_s_memrealtime();
         uint32_t sh0 = cap - hi0;
@@ -471,8 +485,14 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
 #endif
         }
         __syncthreads();   // every lane has read part 0 before part 1 overwrites the buffer's front
-        bin_dma_runs_pf(pdsc, pnxt, nrun / NP + w * (nrun - nrun / NP) / NW, nrun / NP + (w + 1) * (nrun - nrun / NP) / NW,
-                        stage, raw, lo1);
+        if (adma) {
+            bin_dma_runs_asm(pdsc.x, ppk, nrun / NP + w * (nrun - nrun / NP) / NW,
+                             nrun / NP + (w + 1) * (nrun - nrun / NP) / NW, stage, raw, lo1);
+            bin_dma_wait();
+        } else {
+            bin_dma_runs_pf(pdsc, pnxt, nrun / NP + w * (nrun - nrun / NP) / NW,
+                            nrun / NP + (w + 1) * (nrun - nrun / NP) / NW, stage, raw, lo1);
+        }
         __syncthreads();
 #pragma unroll
         for (int t = 0; t < D; ++t) {

@@ -299,6 +299,12 @@ def test_cache_policy_switches_bit_exact(oracle_mod, name, pol):
     ("d32_t5_eps_n50000_sa1024", 1124 | 4096, 1), ("d32_t5_dlpsw_sa2048", 1124 | 4096, 1),
     ("cfg4_shape_2e17", 1124 | 4096, 1), ("d32_avg_clean_sa1024", 1124 | 4096, 1),
     ("faulty_d32_t5_byzrandom_drop_sa1024", 1124 | 4096, 1), ("d32_t5_eps_n50000_sa1024", 1124 | 4096, 0),
+    # run copies by asm saddr LDS-DMA (8192, the default since round 5), with either pick-up; 5220
+    # keeps the compiler's copies
+    ("cfg4_shape_2e17", 5220, 1), ("d32_t5_dlpsw_sa2048", 5220, 1),
+    ("d32_t5_eps_n50000_sa1024", 1124 | 8192, 1), ("d32_t5_eps_n50000_sa1024", 5220 | 8192, 1),
+    ("d32_t5_dlpsw_sa2048", 5220 | 8192, 1), ("cfg4_shape_2e17", 5220 | 8192, 1),
+    ("d32_avg_clean_sa1024", 5220 | 8192, 1), ("faulty_d32_t5_byzrandom_drop_sa1024", 5220 | 8192, 1),
     ("d32_t5_dlpsw_sa2048", 1124, 1), ("cfg4_shape_2e17", 1124, 1),
     ("faulty_d32_t5_byzrandom_drop_sa1024", 1124, 1), ("d32_avg_clean_sa1024", 1124, 1)])
 def test_clamped_pickup_bit_exact(oracle_mod, name, pol, pack):

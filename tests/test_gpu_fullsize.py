@@ -61,10 +61,11 @@ def test_cfg4_full_size_bit_exact(oracle_mod, name, over):
     assert np.array_equal(bits(gt), bits(ot)), "spread traces differ"
 
 
-@pytest.mark.parametrize("pol", [1124, 1124 | 4096])
+@pytest.mark.parametrize("pol", [1124, 1124 | 4096, 5220, 5220 | 8192])
 def test_cfg4_clamped_pickup_matches_golden(pol):
     """The clamped pick-up (ACSIM_BIN_POL bit 1024 with the one-level stores 64), OR-merged (1124)
-    and packed 16-bit (4096, the default since round 5), on the bench workload:
+    and packed 16-bit (4096, the default since round 5), with the compiler's run
+    copies (5220) and the asm saddr ones (8192, the default since round 5), on the bench workload:
     100 FIXED rounds against the committed golden hash, bit for bit."""
     old = os.environ.get("ACSIM_BIN_POL")
     os.environ["ACSIM_BIN_POL"] = str(pol)
