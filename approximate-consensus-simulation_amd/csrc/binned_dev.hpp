@@ -28,7 +28,8 @@ constexpr uint32_t kPolClampPick = 1024; // phase B (NP = 2): pick-up by clamped
 // and removed)
 constexpr uint32_t kPolBytePick = 4096;  // phase B (clamped pick-up, clean plans): packed 16-bit pick-up, add-merged
 constexpr uint32_t kPolAsmDma = 8192;    // phase B (clamped pick-up): run copies by asm saddr LDS-DMA (bin_dma_runs_asm)
-constexpr uint32_t kPolMask = 16383;     // every switch (ACSIM_BIN_POL)
+constexpr uint32_t kPolAsmDmaT = 16384;  // phase M and one-pass phase B: run copies by asm saddr LDS-DMA (bin_dma_runs_asm_tb)
+constexpr uint32_t kPolMask = 32767;     // every switch (ACSIM_BIN_POL)
 // Default switches (the stage-store bits are chosen per plan).  Until round 4 the
 // stream's store flavour was a runtime argument, and the compiler merged the nontemporal and the
 // plain store of its two branches into one plain store: every "nontemporal stage store" measured
@@ -40,10 +41,10 @@ constexpr uint32_t kPolMask = 16383;     // every switch (ACSIM_BIN_POL)
 // 7.60 against 7.86 ms per round for plain ones (the 16 GiB of stages far exceed the MALL)
 constexpr uint32_t kPolOneLevelStores = kPolSc1Store;
 constexpr uint32_t kPolTwoLevelStores = kPolNtStore | kPolNtStoreM;
-constexpr uint32_t kPolDefault = kPolNtInv | kPolBfPick | kPolClampPick | kPolBytePick | kPolAsmDma;   // measured
-// (cfg4): phase B 80 -> 71 (nt invpos) -> 63.2 us (pick-up); the clamped pick-up: round 117.2-118.8 -> 112.3-112.9
-// us; the packed 16-bit pick-up: 112.2-113.0 -> 110.2-111.0 us; the asm run copies: a further
-// -0.4 us (§5.11)
+constexpr uint32_t kPolDefault = kPolNtInv | kPolBfPick | kPolClampPick | kPolBytePick | kPolAsmDma | kPolAsmDmaT;
+// measured (cfg4): phase B 80 -> 71 (nt invpos) -> 63.2 us (pick-up); the clamped pick-up: round 117.2-118.8 ->
+// 112.3-112.9 us; the packed 16-bit pick-up: 112.2-113.0 -> 110.2-111.0 us; the asm run copies:
+// a further -0.4 us, and cfg4 fp32 (one-pass phase B) 79.0 -> 76.8 us (§5.11)
 
 // ------------------------------------------------------------------------------ shared pieces
 // Stream [p0, p1) of an index stream: out[p] = lds[idx[p]].  Super-steps of 512 positions per
@@ -366,6 +367,46 @@ __device__ __forceinline__ void bin_dma_runs_asm(uint32_t so_l, uint32_t pk_l, u
             if (lane < n16 - o)
                 asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
                              :: "v"(voff), "s"(sb + o * 16u), "s"(m0 + o * 16u) : "memory");
+    }
+#endif
+}
+// bin_dma_runs with asm copies (kPolAsmDmaT): descriptors fetched one per lane, 64 at a time, as
+// there; each run's stage address in an SGPR pair and its LDS destination in M0 (bin_dma_runs_asm).
+// The caller waits with bin_dma_wait before the barrier that publishes the image.
+template <bool NT, typename VT = double>
+__device__ __forceinline__ void bin_dma_runs_asm_tb(const uint2* __restrict__ tb, uint32_t r0, uint32_t r1,
+                                                    const VT* __restrict__ src, VT* dst, uint32_t base = 0) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    constexpr uint32_t EPU = 16 / sizeof(VT);
+    const uint32_t lane = threadIdx.x & 63, voff = lane * 16u;
+    const uint32_t lb = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)dst;
+    for (uint32_t g = r0; g < r1; g += 64) {
+        const uint32_t ng = r1 - g < 64 ? r1 - g : 64;
+        uint2 dsc = make_uint2(0u, 0u);
+        uint32_t nxt = 0;
+        if (lane < ng) {
+            dsc = tb[g + lane];
+            nxt = tb[g + lane + 1].y;
+        }
+        // the descriptors' wait, here: left to the compiler it sits in the run loop's header, where
+        // (blind to the asm copies) it waits for every copy issued so far, once per run
+        asm volatile("" : "+v"(dsc.x), "+v"(dsc.y), "+v"(nxt));
+        for (uint32_t k = 0; k < ng; ++k) {
+            const uint32_t so = __builtin_amdgcn_readlane(dsc.x, k) & ~(EPU - 1u);   // low bits: pad count
+            const uint32_t pre = __builtin_amdgcn_readlane(dsc.y, k);
+            const uint32_t n16 = (__builtin_amdgcn_readlane(nxt, k) - pre) / EPU;
+            const uint64_t sb = (uint64_t)(uintptr_t)src + (uint64_t)so * sizeof(VT);
+            const uint32_t m0 = lb + (pre - base) * (uint32_t)sizeof(VT);
+            for (uint32_t o = 0; o < n16; o += 64)
+                if (lane < n16 - o) {
+                    if constexpr (NT)
+                        asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 nt"
+                                     :: "v"(voff), "s"(sb + o * 16u), "s"(m0 + o * 16u) : "memory");
+                    else
+                        asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+                                     :: "v"(voff), "s"(sb + o * 16u), "s"(m0 + o * 16u) : "memory");
+                }
+        }
     }
 #endif
 }

@@ -178,7 +178,12 @@ __global__ __launch_bounds__(kBinA) void k_bin_regroup(const VT* __restrict__ st
     const uint32_t g = blockIdx.x;
     constexpr uint32_t NW = kBinA / 64;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    bin_dma_runs(mt + (uint64_t)g * (PK + 1), w * PK / NW, (w + 1) * PK / NW, stage1, lm);
+    if (pol & kPolAsmDmaT) {
+        bin_dma_runs_asm_tb<false>(mt + (uint64_t)g * (PK + 1), w * PK / NW, (w + 1) * PK / NW, stage1, lm);
+        bin_dma_wait();
+    } else {
+        bin_dma_runs(mt + (uint64_t)g * (PK + 1), w * PK / NW, (w + 1) * PK / NW, stage1, lm);
+    }
     __syncthreads();
     const uint64_t t1 = ts ? __builtin_amdgcn_s_memrealtime() : 0;
     bin_stream(lm, idxM, stage2, moff[g], moff[g + 1], (pol & kPolSc1StoreM) ? 2u : (pol & kPolNtStoreM) ? 1u : 0u);
@@ -398,7 +403,15 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
     }
     VT v[D + 1];
     if constexpr (NP == 1) {
-        bin_dma_runs(tb, w * nrun / NW, (w + 1) * nrun / NW, stage, raw, (pol & kPolNtRuns) != 0);
+        if (pol & kPolAsmDmaT) {
+            if (pol & kPolNtRuns)
+                bin_dma_runs_asm_tb<true>(tb, w * nrun / NW, (w + 1) * nrun / NW, stage, raw);
+            else
+                bin_dma_runs_asm_tb<false>(tb, w * nrun / NW, (w + 1) * nrun / NW, stage, raw);
+            bin_dma_wait();
+        } else {
+            bin_dma_runs(tb, w * nrun / NW, (w + 1) * nrun / NW, stage, raw, (pol & kPolNtRuns) != 0);
+        }
         __syncthreads();
         if (a.ts) t1 = __builtin_amdgcn_s_memrealtime();
 #pragma unroll

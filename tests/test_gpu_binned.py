@@ -292,6 +292,24 @@ def test_cache_policy_switches_bit_exact(oracle_mod, name, pol):
         assert np.array_equal(rb, o.rounds()) and np.array_equal(xb, bits(o.values(0)))
 
 
+@pytest.mark.parametrize("name,pol", [
+    ("two_level_d16_t5_n100000_sa256", 16384), ("two_level_d16_t5_n100000_sa256", 16384 | 130),
+    ("two_level_d32_mid_n150001_sa512", 16384 | 1), ("faulty_two_level_d16_t5_crash_drop_sa256", 16384),
+    ("d16_t5_fixed_odd_sa512", 16384 | 1), ("d8_t2_midpoint_sa256", 16384),
+    ("d32_t5_eps_n50000_sa1024", 16384 | 1), ("faulty_d16_avg_drop_sa512", 16384)])
+def test_asm_run_copies_phase_m_and_one_pass_bit_exact(oracle_mod, name, pol):
+    """Run copies by asm saddr LDS-DMA in phase M and in the one-pass phase B (ACSIM_BIN_POL bit
+    16384, bin_dma_runs_asm_tb; plain and nontemporal), on one- and two-level, clean and faulty
+    plans, against the oracle bit for bit."""
+    cfg, sa = CASES[name]
+    with env(ACSIM_BIN_SA=sa, ACSIM_BIN_POL=pol, ACSIM_BIN_SPLIT=1):
+        kb, rb, xb, tb = run_gpu(cfg)
+    assert " split2" not in kb, kb
+    with oracle_mod.OracleSimulator(cfg, threads=8) as o:
+        o.run()
+        assert np.array_equal(rb, o.rounds()) and np.array_equal(xb, bits(o.values(0)))
+
+
 @pytest.mark.parametrize("name,pol,pack", [
     ("d32_t5_eps_n50000_sa1024", 1124, 1), ("d32_t5_eps_n50000_sa1024", 1060, 1),
     # the packed 16-bit pick-up (4096, the default since round 5; DESIGN.md §5.11); the faulty plan
