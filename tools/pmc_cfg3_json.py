@@ -43,7 +43,7 @@ for k, cs in acc.items():
     kern[k] = m
 lib = os.path.join(ROOT, "approximate-consensus-simulation_amd", "acsim", "_lib", "libacsim.so")
 rec = {"source": "tools/pmc_cfg3.sh (rocprofv3 --pmc, 3 passes) over tools/bench_configs.py cfg3 cfg3_g16",
-       "derivation": __doc__.split("\n\n")[1].strip(),
+       "derivation": " ".join(__doc__.split("\n\n")[2].split()),
        "lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),
        "src_sha256": __import__("bench").src_sha256(),
        "kernels": kern}
