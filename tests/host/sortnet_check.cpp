@@ -1,6 +1,7 @@
 // Host check of csrc/sortnet.hpp (compiled with g++ by tests/test_sortnet_host.py):
 //  1. every selection network the register kernels instantiate (M = d + 1 entries, window [t, M - t))
-//     puts the window's order statistics where std::sort does, on random multisets with ties;
+//     puts the window's order statistics where std::sort does, on random multisets with ties, and
+//     passes the 0-1 principle (exhaustively up to 17 entries, sampled at 33);
 //  2. the NZ tree sum (padding adds skipped, one final +0.0) equals the spec's tree bit for bit,
 //     signed zeros and denormals included.
 #include <algorithm>
@@ -34,6 +35,49 @@ static long check_net(std::mt19937_64& g, int iters) {
     return bad;
 }
 
+// 0-1 principle, 64 inputs per word: every 0-1 vector (M <= 20) or `samples` random words of them
+// (with every density of ones) through the pruned network and its output permutation; the
+// window must hold the sorted vector's ones and zeros.
+template <int M, int LO, int HI>
+static long check_01(std::mt19937_64& g, long samples) {
+    using Net = SelectNet<M, LO, HI>;
+    const bool all = M <= 20;
+    const long words = all ? ((1L << M) + 63) / 64 : samples;
+    long bad = 0;
+    for (long w = 0; w < words; ++w) {
+        uint64_t x[M];
+        if (all) {
+            for (int k = 0; k < M; ++k) {
+                uint64_t m = 0;
+                for (int j = 0; j < 64; ++j) m |= (uint64_t)(((w * 64 + j) >> k) & 1) << j;
+                x[k] = m;
+            }
+        } else {
+            const int dens = (int)(w % (M + 1));   // P(one) = dens / M
+            for (int k = 0; k < M; ++k) {
+                uint64_t m = 0;
+                for (int j = 0; j < 64; ++j) m |= (uint64_t)((int)(g() % M) < dens) << j;
+                x[k] = m;
+            }
+        }
+        int ones[64] = {};
+        for (int k = 0; k < M; ++k)
+            for (int j = 0; j < 64; ++j) ones[j] += (int)((x[k] >> j) & 1);
+        for (int q = 0; q < Net::count; ++q) {
+            const int a = Net::list.c[q].a, b = Net::list.c[q].b;
+            const uint64_t lo = x[a] & x[b], hi = x[a] | x[b];
+            x[a] = lo;
+            x[b] = hi;
+        }
+        for (int k = LO; k < HI; ++k) {
+            const uint64_t got = x[Net::net.perm[k]];
+            for (int j = 0; j < 64; ++j)
+                bad += (int)((got >> j) & 1) != (k >= M - ones[j] ? 1 : 0);
+        }
+    }
+    return bad;
+}
+
 template <int N, int OFF, int STRIDE, int M>
 static long check_tree(const double (&a)[M]) {
     return bits(tree_sum_const<N, OFF, STRIDE, false>(a)) != bits(tree_sum_const<N, OFF, STRIDE, true>(a));
@@ -48,6 +92,11 @@ int main() {
     bad += check_net<17, 0, 17>(g, 100000);
     bad += check_net<9, 2, 7>(g, 100000);     // d = 8, t = 2
     bad += check_net<5, 1, 4>(g, 100000);     // d = 4, t = 1
+    bad += check_01<17, 0, 17>(g, 0);         // every 0-1 vector: Green's network + insertion
+    bad += check_01<17, 5, 12>(g, 0);
+    bad += check_01<9, 2, 7>(g, 0);
+    bad += check_01<33, 5, 28>(g, 60000);     // 3.8 M random 0-1 vectors, all densities
+    bad += check_01<33, 0, 33>(g, 60000);
     long nbad_net = bad;
     const double pool[] = {0.0, -0.0, 5e-324, -5e-324, 1.0, -1.0, 0.5, -0.5, 1e-310, -1e-310, 3.0, -3.0};
     long ntree = 0;
