@@ -96,6 +96,9 @@ struct acs_sim {
     bool want_summary = false;     // acs_run on a one-launch path: enqueue the summary before the sync
     bool summary_ready = false;    // h_sum holds the summary of the current state
     unsigned long long sum_seq = 0;    // sequence number of the last summary launch (h_sum->seq)
+    MappedStates* h_ms = nullptr;      // pinned, host-mapped instance states (B <= kMappedStates), or null
+    MappedStates* h_ms_dev = nullptr;  // its device address
+    unsigned long long ms_seq = 0;     // sequence number of the last launch_states_mapped
     uint32_t round = 0;            // round of every unfinished instance
     bool all_done = false;
     // node partitioning: rank owns rows [rank*rows_per, (rank+1)*rows_per) ∩ [0, N)
@@ -286,6 +289,7 @@ static void release(acs_sim* s) {
     if (s->h_ndone) (void)hipHostFree(s->h_ndone);
     (void)hipFree(s->sum_scratch);
     if (s->h_sum) (void)hipHostFree(s->h_sum);
+    if (s->h_ms) (void)hipHostFree(s->h_ms);
     if (s->eacc) (void)hipFree(s->eacc);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
@@ -696,8 +700,36 @@ static int enqueue_round(acs_sim* s, uint32_t r) {
     return ACS_OK;
 }
 
+// Poll a host-mapped sequence number a launch on s->stream releases at system scope.  The stream is
+// queried every 256 spins, so a failed launch returns its error rather than spinning forever.
+static int wait_mapped_seq(acs_sim* s, const unsigned long long* p, unsigned long long seq, const char* what) {
+    for (uint32_t it = 1;; ++it) {
+        if (__atomic_load_n(p, __ATOMIC_ACQUIRE) == seq) return ACS_OK;
+        if ((it & 255u) == 0) {
+            const hipError_t q = hipStreamQuery(s->stream);
+            if (q == hipSuccess) {
+                if (__atomic_load_n(p, __ATOMIC_ACQUIRE) == seq) return ACS_OK;
+                return fail(ACS_EDEVICE, "%s: stream idle without the sequence number", what);
+            }
+            if (q != hipErrorNotReady) return fail(ACS_EDEVICE, "%s: %s", what, hipGetErrorString(q));
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+// The B instance states after everything enqueued so far.  Handles of at most kMappedStates
+// instances take them through host-mapped memory (launch_states_mapped: no device-to-host copy,
+// no wait on the stream's completion signal); the stream may still be retiring that small launch
+// on return, and later work stays ordered behind it.
 static int read_states(acs_sim* s, std::vector<InstState>& out) {
     out.resize(s->B);
+    if (s->h_ms) {
+        const unsigned long long seq = ++s->ms_seq;
+        HIP_TRY(launch_states_mapped(s->st, (uint32_t)s->B, s->h_ms_dev, seq, s->stream));
+        if (int rc = wait_mapped_seq(s, &s->h_ms->seq, seq, "instance states")) return rc;
+        memcpy(out.data(), s->h_ms->st, s->B * sizeof(InstState));
+        return ACS_OK;
+    }
     HIP_TRY(hipMemcpyAsync(out.data(), s->st, s->B * sizeof(InstState), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     return ACS_OK;
@@ -713,18 +745,7 @@ static constexpr uint32_t kChunk = 16;
 static int summary_and_wait(acs_sim* s) {
     const unsigned long long seq = ++s->sum_seq;
     HIP_TRY(launch_run_summary_mapped(s->st, s->B, s->sum_scratch, s->h_sum_dev, seq, s->stream));
-    for (uint32_t it = 1;; ++it) {
-        if (__atomic_load_n(&s->h_sum->seq, __ATOMIC_ACQUIRE) == seq) return ACS_OK;
-        if ((it & 255u) == 0) {
-            const hipError_t q = hipStreamQuery(s->stream);
-            if (q == hipSuccess) {
-                if (__atomic_load_n(&s->h_sum->seq, __ATOMIC_ACQUIRE) == seq) return ACS_OK;
-                return fail(ACS_EDEVICE, "run summary: stream idle without the summary's sequence number");
-            }
-            if (q != hipErrorNotReady) return fail(ACS_EDEVICE, "run summary: %s", hipGetErrorString(q));
-        }
-        __builtin_ia32_pause();
-    }
+    return wait_mapped_seq(s, &s->h_sum->seq, seq, "run summary");
 }
 
 // Launch a finalize still deferred (the last round enqueued has no next phase A to fold it).
@@ -1100,6 +1121,11 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     CREATE_TRY(hipHostMalloc(&s->h_sum, sizeof(RunSummary), hipHostMallocMapped | hipHostMallocPortable));
     CREATE_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&s->h_sum_dev), s->h_sum, 0));
     memset(s->h_sum, 0, sizeof(RunSummary));
+    if (s->B <= kMappedStates) {
+        CREATE_TRY(hipHostMalloc(&s->h_ms, sizeof(MappedStates), hipHostMallocMapped | hipHostMallocPortable));
+        CREATE_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&s->h_ms_dev), s->h_ms, 0));
+        memset(s->h_ms, 0, sizeof(MappedStates));
+    }
     CREATE_TRY(hipMalloc(&s->sum_scratch, kSummaryScratch));
     {
         const char* v = getenv("ACSIM_EPS_PUB");

@@ -146,6 +146,17 @@ struct RunSummary {   // acs_run's result, folded on the device (40 bytes)
 // launch's sequence number), so the host may read them once it sees `seq` without waiting for the
 // stream's completion signal.
 constexpr uint32_t kSummaryScratch = 1024 * 48 + 64;
+// Instance states read back through host-mapped memory (acs_round's info and the state getters on
+// handles of at most kMappedStates instances): one small launch copies them and then releases a
+// sequence number at system scope, and the host polls that number instead of a device-to-host copy
+// and the stream's completion signal.
+constexpr uint32_t kMappedStates = 16;
+struct MappedStates {
+    InstState st[kMappedStates];
+    unsigned long long seq;   // stored last (system-scope release)
+};
+hipError_t launch_states_mapped(const InstState* st, uint32_t B, MappedStates* out, unsigned long long seq,
+                                hipStream_t s);
 hipError_t launch_run_summary_mapped(const InstState* st, uint64_t B, void* scratch, RunSummary* out,
                                      unsigned long long seq, hipStream_t s);
 

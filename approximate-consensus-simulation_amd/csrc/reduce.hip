@@ -134,6 +134,21 @@ hipError_t launch_run_summary_mapped(const InstState* st, uint64_t B, void* scra
     return hipGetLastError();
 }
 
+// One thread copies the B <= kMappedStates states (its own stores, so the release below orders them)
+__global__ __launch_bounds__(64) void k_states_mapped(const InstState* __restrict__ st, uint32_t B,
+                                                      MappedStates* out, unsigned long long seq) {
+    if (threadIdx.x != 0) return;
+    for (uint32_t b = 0; b < B; ++b) out->st[b] = st[b];
+    __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_states_mapped(const InstState* st, uint32_t B, MappedStates* out, unsigned long long seq,
+                                hipStream_t s) {
+    if (B > kMappedStates) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_states_mapped, dim3(1), dim3(64), 0, s, st, B, out, seq);
+    return hipGetLastError();
+}
+
 hipError_t launch_partials_from_x(const double* x, const uint32_t* status, uint64_t B, uint64_t N,
                                   double2* partial, uint32_t nblk, bool f32, hipStream_t s) {
     if (f32)
