@@ -99,6 +99,7 @@ struct acs_sim {
     MappedStates* h_ms = nullptr;      // pinned, host-mapped instance states (B <= kMappedStates), or null
     MappedStates* h_ms_dev = nullptr;  // its device address
     unsigned long long ms_seq = 0;     // sequence number of the last launch_states_mapped
+    bool ms_fresh = false;             // h_ms holds the states advance() ended with (acs_round reuses them)
     uint32_t round = 0;            // round of every unfinished instance
     bool all_done = false;
     // node partitioning: rank owns rows [rank*rows_per, (rank+1)*rows_per) ∩ [0, N)
@@ -721,12 +722,32 @@ static int wait_mapped_seq(acs_sim* s, const unsigned long long* p, unsigned lon
 // instances take them through host-mapped memory (launch_states_mapped: no device-to-host copy,
 // no wait on the stream's completion signal); the stream may still be retiring that small launch
 // on return, and later work stays ordered behind it.
-static int read_states(acs_sim* s, std::vector<InstState>& out) {
+static int fetch_mapped_states(acs_sim* s) {
+    const unsigned long long seq = ++s->ms_seq;
+    HIP_TRY(launch_states_mapped(s->st, s->n_done, (uint32_t)s->B, s->h_ms_dev, seq, s->stream));
+    return wait_mapped_seq(s, &s->h_ms->seq, seq, "instance states");
+}
+
+// The done count after everything enqueued so far (EPS chunks and call ends): through the mapped
+// states where the handle has them (which then hold the states of that moment too).
+static int fetch_done_count(acs_sim* s, uint32_t& nd) {
+    if (s->h_ms) {
+        if (int rc = fetch_mapped_states(s)) return rc;
+        nd = s->h_ms->n_done;
+        return ACS_OK;
+    }
+    HIP_TRY(hipMemcpyAsync(s->h_ndone, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    nd = s->h_ndone[0];
+    return ACS_OK;
+}
+
+static int read_states(acs_sim* s, std::vector<InstState>& out, bool reuse_fresh = false) {
     out.resize(s->B);
     if (s->h_ms) {
-        const unsigned long long seq = ++s->ms_seq;
-        HIP_TRY(launch_states_mapped(s->st, (uint32_t)s->B, s->h_ms_dev, seq, s->stream));
-        if (int rc = wait_mapped_seq(s, &s->h_ms->seq, seq, "instance states")) return rc;
+        if (!(reuse_fresh && s->ms_fresh))
+            if (int rc = fetch_mapped_states(s)) return rc;
+        s->ms_fresh = false;
         memcpy(out.data(), s->h_ms->st, s->B * sizeof(InstState));
         return ACS_OK;
     }
@@ -765,6 +786,7 @@ struct RoctxRange {
 
 // Advance every unfinished instance by at most k rounds.
 static int advance(acs_sim* s, uint32_t k) {
+    s->ms_fresh = false;
     if (s->all_done || k == 0) return ACS_OK;
     const uint32_t cap = s->c.max_rounds > s->round ? s->c.max_rounds - s->round : 0;
     if (k > cap) k = cap;
@@ -834,9 +856,9 @@ static int advance(acs_sim* s, uint32_t k) {
         k -= chunk;
         if (s->round >= s->c.max_rounds) break;
         if (sync_poll && k > 0) {
-            HIP_TRY(hipMemcpyAsync(s->h_ndone, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
-            HIP_TRY(hipStreamSynchronize(s->stream));
-            if (s->h_ndone[0] == s->B) s->all_done = true;
+            uint32_t nd = 0;
+            if (int rc = fetch_done_count(s, nd)) return rc;
+            if (nd == s->B) s->all_done = true;
         } else if (eps_mode && !sync_poll) {
             // keep one chunk in flight: poll the previous chunk's done counter
             HIP_TRY(hipMemcpyAsync(s->h_ndone + slot, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost,
@@ -862,9 +884,16 @@ static int advance(acs_sim* s, uint32_t k) {
         s->all_done = s->round >= s->c.max_rounds;
         return ACS_OK;
     }
-    HIP_TRY(hipMemcpyAsync(s->h_ndone, s->n_done, sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
-    HIP_TRY(hipStreamSynchronize(s->stream));
-    s->all_done = s->h_ndone[0] == s->B;
+    if (s->want_summary) {   // acs_run: the summary carries the done count (one round trip, not two)
+        if (int rc = summary_and_wait(s)) return rc;
+        s->summary_ready = true;
+        s->all_done = s->h_sum->n_done == s->B;
+        return ACS_OK;
+    }
+    uint32_t nd = 0;
+    if (int rc = fetch_done_count(s, nd)) return rc;
+    s->ms_fresh = s->h_ms != nullptr;   // nothing is enqueued after it: acs_round reuses these states
+    s->all_done = nd == s->B;
     return ACS_OK;
 }
 
@@ -1435,7 +1464,7 @@ int acs_round(acs_sim* s, uint32_t k, acs_round_info* out) {
     int rc = advance(s, k);
     if (rc) return rc;
     std::vector<InstState> v;
-    rc = read_states(s, v);
+    rc = read_states(s, v, true);   // (EPS calls end with the states already fetched)
     if (rc) return rc;
     fill_info(s, v, out);
     return ACS_OK;

@@ -153,10 +153,11 @@ constexpr uint32_t kSummaryScratch = 1024 * 48 + 64;
 constexpr uint32_t kMappedStates = 16;
 struct MappedStates {
     InstState st[kMappedStates];
+    uint32_t n_done, pad;     // the device's count of done instances
     unsigned long long seq;   // stored last (system-scope release)
 };
-hipError_t launch_states_mapped(const InstState* st, uint32_t B, MappedStates* out, unsigned long long seq,
-                                hipStream_t s);
+hipError_t launch_states_mapped(const InstState* st, const uint32_t* n_done, uint32_t B, MappedStates* out,
+                                unsigned long long seq, hipStream_t s);
 hipError_t launch_run_summary_mapped(const InstState* st, uint64_t B, void* scratch, RunSummary* out,
                                      unsigned long long seq, hipStream_t s);
 

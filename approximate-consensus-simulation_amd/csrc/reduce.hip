@@ -135,17 +135,19 @@ hipError_t launch_run_summary_mapped(const InstState* st, uint64_t B, void* scra
 }
 
 // One thread copies the B <= kMappedStates states (its own stores, so the release below orders them)
-__global__ __launch_bounds__(64) void k_states_mapped(const InstState* __restrict__ st, uint32_t B,
+__global__ __launch_bounds__(64) void k_states_mapped(const InstState* __restrict__ st,
+                                                      const uint32_t* __restrict__ n_done, uint32_t B,
                                                       MappedStates* out, unsigned long long seq) {
     if (threadIdx.x != 0) return;
     for (uint32_t b = 0; b < B; ++b) out->st[b] = st[b];
+    out->n_done = *n_done;
     __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-hipError_t launch_states_mapped(const InstState* st, uint32_t B, MappedStates* out, unsigned long long seq,
-                                hipStream_t s) {
+hipError_t launch_states_mapped(const InstState* st, const uint32_t* n_done, uint32_t B, MappedStates* out,
+                                unsigned long long seq, hipStream_t s) {
     if (B > kMappedStates) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_states_mapped, dim3(1), dim3(64), 0, s, st, B, out, seq);
+    hipLaunchKernelGGL(k_states_mapped, dim3(1), dim3(64), 0, s, st, n_done, B, out, seq);
     return hipGetLastError();
 }
 
