@@ -49,6 +49,10 @@ static int fail(int code, const char* fmt, ...) {
 
 enum Path { PATH_REGULAR = 0, PATH_GENERIC = 1, PATH_BATCHED = 2, PATH_DENSE = 3 };
 
+// CSR plans (and hub rows beside them) share one partial-slot numbering between the binned phase B
+// and the per-lane / generic kernels: their receiver blocks must agree.
+static_assert(kBinSB == kRegularBlock, "CSR binned plans index partials by kRegularBlock-row blocks");
+
 struct Part {              // one node partition's private copy (virtual partitions only)
     double* x[2] = {nullptr, nullptr};
     uint32_t* ell = nullptr;
@@ -474,7 +478,7 @@ static int enqueue_round_xchunked(acs_sim* s, uint32_t r) {
     const uint64_t cs = s->rows_per / K;
     const uint32_t SA = s->bin_sa;
     const uint32_t bpr = (uint32_t)(s->rows_per / SA), bpc = (uint32_t)(cs / SA);
-    const uint32_t qpc = (uint32_t)(cs / kBinSB);
+    const uint32_t qpc = (uint32_t)(cs / s->bin.SB);   // phase-B receiver blocks per chunk
     const int nparts = s->virt ? s->nranks : 1;
     auto pargs = [&](int p) {
         RoundArgs ap = a;
@@ -1075,22 +1079,26 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     // a tested variant
     std::string kname_lane;   // (set with the binned decision below)
     const char* of_env = getenv("ACSIM_BIN_OF");
-    // (rid is one byte per entry: receiver blocks of at most 256)
-    const bool bin_of = s->ell_sorted && of_env && of_env[0] == '1' && !s->csr_var && kBinSB <= 256;
+    // (rid is one byte per entry: receiver blocks of kBinSB = 256)
+    const bool bin_of = s->ell_sorted && of_env && of_env[0] == '1' && !s->csr_var;
+    // phase-B receiver block (BinnedPlan::SB): the default, or ACSIM_BIN_SB where the clean (d, t)
+    // pair has that instantiation; block partials follow it (one per receiver block)
+    const uint32_t bin_sb = binned_block_size(s->d, cfg->trim, cfg->rule,
+                                              s->clean && !s->csr_var && !bin_of && s->path == PATH_REGULAR);
     {
         const char* env = getenv("ACSIM_BINNED");
         const bool allow = !(env && env[0] == '0');
-        const uint32_t lv = s->path == PATH_REGULAR && s->d ? binned_levels(s->N, rows_local, s->d, bin_sa, nullptr) : 0;
+        const uint32_t lv =
+            s->path == PATH_REGULAR && s->d ? binned_levels(s->N, rows_local, s->d, bin_sa, bin_sb, nullptr) : 0;
         // fp32 tags carry a 20-bit sender field: above 2^20 nodes a crash schedule stores crash ranks
         // there (at most 2^20 senders may crash in one round: n_faulty <= 2^20)
         const bool f32_tags_ok = !s->f32 || s->clean || s->N <= (1ull << 20) || cfg->fault_model != ACS_FAULT_CRASH ||
                                  cfg->n_faulty <= (1u << 20);
         s->binned = allow && f32_tags_ok && s->path == PATH_REGULAR && cfg->delay_max == 0 &&
                     !(s->csr_var && s->f32) &&
-                    // CSR hub rows own the partial slots after the fast path's kRegularBlock-row
-                    // blocks, and phase B writes slot b for its kBinSB-row block b: the two block
-                    // sizes must agree (an ACS_BIN_SB variant build keeps hub graphs per-lane)
-                    !(s->n_hub && kBinSB != kRegularBlock) &&
+                    // (CSR hub rows own the partial slots after the fast path's blocks; CSR plans
+                    // always take kBinSB = kRegularBlock receivers per block, so both paths agree:
+                    // static_assert below)
                     s->B == 1 && lv != 0 &&
                     binned_supported(s->d, cfg->trim, cfg->rule) && rows_local * s->d < (1ull << 32);
         const char* df = getenv("ACSIM_DEFER_FIN");
@@ -1102,11 +1110,19 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
                      cfg->trim, s->clean ? "" : ",faulty", s->csr_var ? ",csr" : "",
                      cfg->fault_model != ACS_FAULT_NONE ? "+k_bin_tag" : "");
             s->kname = nm;
+            if (bin_sb != kBinSB) s->kname += " sb" + std::to_string(bin_sb);
         }
     }
     if (s->n_hub) s->kname += "+k_round_generic(hubs)";
     if (s->f32) s->kname += " [f32]";
-    s->nblk = s->path == PATH_REGULAR ? (uint32_t)((rows_local + kRegularBlock - 1) / kRegularBlock)
+    // Block partials: one per receiver block of the round kernel.  The binned path's phase B writes
+    // slot b of its bin_sb-row block b, the per-lane kernel slot b of its kRegularBlock-row block b;
+    // a binned plan refused below falls back to the per-lane kernel, so the buffer holds the larger
+    // count and nblk is reset to the per-lane count on that fallback (launch_round_binned refuses a
+    // plan whose block count exceeds nblk).
+    const uint32_t nblk_lane = (uint32_t)((rows_local + kRegularBlock - 1) / kRegularBlock);
+    const uint32_t nblk_bin = (uint32_t)((rows_local + bin_sb - 1) / bin_sb);
+    s->nblk = s->path == PATH_REGULAR ? (s->binned ? nblk_bin : nblk_lane)
             : s->path == PATH_GENERIC ? (uint32_t)s->N
             : s->path == PATH_DENSE   ? dense_nblk(s->N)
                                       : 0u;
@@ -1114,7 +1130,10 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     s->nblk += (uint32_t)s->n_hub;   // hub rows: one partial slot each, after the fast path's
     s->nblk_init = (uint32_t)((s->N + 255) / 256);
     if (s->nblk_init > 1024) s->nblk_init = 1024;
-    const uint64_t nround = (uint64_t)s->nblk * (virt ? nranks : 1);
+    const uint32_t nblk_max = s->path == PATH_REGULAR ? (nblk_bin > nblk_lane ? nblk_bin : nblk_lane) + (uint32_t)s->n_hub
+                                                      : s->nblk;
+    // (virtual partitions: partition p's slice starts at p * nblk, with nblk the count in use)
+    const uint64_t nround = (uint64_t)nblk_max * (virt ? nranks : 1);
     const uint64_t ncap = nround > s->nblk_init ? nround : s->nblk_init;
 
 #define CREATE_TRY(expr)                                                                      \
@@ -1208,8 +1227,8 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         bool bin_refused = false;
         auto try_plan = [&](BinnedPlan& plan, const uint32_t* ell, uint64_t nr) -> hipError_t {
             if (!s->binned || bin_refused || !nr) return hipSuccess;
-            hipError_t e = binned_build(plan, ell, s->N, nr, s->d, s->dp, bin_sa, tagged, s->f32, bin_of, s->stream,
-                                        false, s->status, s->clean);
+            hipError_t e = binned_build(plan, ell, s->N, nr, s->d, s->dp, bin_sa, bin_sb, tagged, s->f32, bin_of,
+                                        s->stream, false, s->status, s->clean);
             if (e == hipErrorNotSupported) {
                 bin_refused = true;
                 return hipSuccess;
@@ -1235,6 +1254,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
             s->binned = false;
             s->defer_fin = false;
             s->kname = kname_lane + (s->f32 ? " [f32]" : "");
+            s->nblk = s->nblk_fast = nblk_lane;   // the per-lane kernel's blocks (no hub rows here)
         }
         if (s->binned) {
             // NP-pass phase B (slot-dependent configs: fp64, two passes only; see launch_round_binned)
@@ -1269,13 +1289,15 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
             CREATE_TRY(launch_csr_to_ell(s->rowptr, s->colidx, s->N, s->d, s->ell, s->deg, s->sw, s->stream));
             if (s->ell_sorted) CREATE_TRY(launch_sort_ell_rows(s->ell, s->N, s->d, s->stream));
             if (s->binned) {
-                const hipError_t be = binned_build(s->bin, s->ell, s->N, s->N, s->d, s->dp, bin_sa, tagged, s->f32, false,
-                                                   s->stream, true, s->status);
+                const hipError_t be = binned_build(s->bin, s->ell, s->N, s->N, s->d, s->dp, bin_sa, kBinSB, tagged,
+                                                   s->f32, false, s->stream, true, s->status);
                 if (be == hipErrorNotSupported) {   // the plan does not fit: the per-lane kernel serves the rows
                     binned_free(s->bin);
                     s->binned = false;
                     s->defer_fin = false;
                     s->kname = kname_lane + (s->n_hub ? "+k_round_generic(hubs)" : "") + (s->f32 ? " [f32]" : "");
+                    s->nblk_fast = nblk_lane;   // (equal to nblk_bin: CSR plans use kBinSB = kRegularBlock)
+                    s->nblk = nblk_lane + (uint32_t)s->n_hub;
                 } else {
                     CREATE_TRY(be);
                     (void)hipFree(s->ell);
@@ -1341,7 +1363,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         uint32_t K = (comm_id && nranks > 1) ? 0u : 4u;
         if (const char* v = getenv("ACSIM_XCHUNKS")) K = (uint32_t)strtoul(v, nullptr, 10);
         if (K >= 2 && K <= acs_sim::kMaxX && s->rows_per % ((uint64_t)K * bin_sa) == 0 &&
-            (s->rows_per / K) % kBinSB == 0)
+            (s->rows_per / K) % s->bin.SB == 0)
             s->xchunks = K;
     }
     s->bin_sa = bin_sa;

@@ -344,6 +344,27 @@ __device__ __forceinline__ void bin_dma_runs_pf(uint2 dsc, uint32_t nxt, uint32_
     }
 }
 
+// One `global_load_lds_dwordx4 voffset, sbase` with its LDS destination in M0.  The compiler treats
+// M0 as a reserved register and does not model an asm write to it (a clobber entry is "undefined
+// behaviour" to LLVM), so the statement saves the compiler's M0 into a scratch SGPR first and
+// restores it after the issue: whatever M0 value the compiler's own LDS-DMA or M0-indexed code
+// holds across the statement is preserved by construction.  (The instruction reads M0 at issue,
+// so rewriting it right after is safe: consecutive copies already rewrite it back to back.)
+template <bool NT>
+__device__ __forceinline__ void bin_lds_dma16(uint32_t voff, uint64_t sbase, uint32_t m0) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t saved;
+    if constexpr (NT)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(saved) : "v"(voff), "s"(sbase), "s"(m0) : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(saved) : "v"(voff), "s"(sbase), "s"(m0) : "memory");
+#endif
+}
+
 // bin_dma_runs_pf with the copies issued as asm `global_load_lds_dwordx4 voffset, sbase` (kPolAsmDma,
 // DESIGN.md §5.11): the run's stage address is an SGPR pair (stage + start, SALU) and the per-lane
 // offset the fixed lane * 16, and the LDS destination goes to M0 in the same statement, so a run
@@ -364,9 +385,7 @@ __device__ __forceinline__ void bin_dma_runs_asm(uint32_t so_l, uint32_t pk_l, u
         const uint64_t sb = (uint64_t)(uintptr_t)src + (uint64_t)(so & ~(16u / sizeof(VT) - 1u)) * sizeof(VT);
         const uint32_t m0 = lb + (pre - base) * (uint32_t)sizeof(VT);
         for (uint32_t o = 0; o < n16; o += 64)
-            if (lane < n16 - o)
-                asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
-                             :: "v"(voff), "s"(sb + o * 16u), "s"(m0 + o * 16u) : "memory");
+            if (lane < n16 - o) bin_lds_dma16<false>(voff, sb + o * 16u, m0 + o * 16u);
     }
 #endif
 }
@@ -398,14 +417,7 @@ __device__ __forceinline__ void bin_dma_runs_asm_tb(const uint2* __restrict__ tb
             const uint64_t sb = (uint64_t)(uintptr_t)src + (uint64_t)so * sizeof(VT);
             const uint32_t m0 = lb + (pre - base) * (uint32_t)sizeof(VT);
             for (uint32_t o = 0; o < n16; o += 64)
-                if (lane < n16 - o) {
-                    if constexpr (NT)
-                        asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 nt"
-                                     :: "v"(voff), "s"(sb + o * 16u), "s"(m0 + o * 16u) : "memory");
-                    else
-                        asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
-                                     :: "v"(voff), "s"(sb + o * 16u), "s"(m0 + o * 16u) : "memory");
-                }
+                if (lane < n16 - o) bin_lds_dma16<NT>(voff, sb + o * 16u, m0 + o * 16u);
         }
     }
 #endif
@@ -427,7 +439,7 @@ __device__ __forceinline__ void bin_ts(uint64_t* ts, uint64_t t0, uint64_t t1) {
 // [k*nrun/NP, (k+1)*nrun/NP)) through an LDS buffer of kBinPartCap<D, NP> elements; after each
 // part's DMA every lane picks up the values whose invpos falls in that part.  1/NP of the LDS per
 // workgroup: more resident workgroups per CU.  The plan enables it only when every part fits.
-template <int D, int NP>
-constexpr uint32_t kBinPartCap = D * kBinSB / NP + D * kBinSB / 16;   // + 1/16 of the image: run-length variation and padding
+template <int D, int NP, int SB = (int)kBinSB>
+constexpr uint32_t kBinPartCap = D * SB / NP + D * SB / 16;   // + 1/16 of the image: run-length variation and padding
 
 }  // namespace acs

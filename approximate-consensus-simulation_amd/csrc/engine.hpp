@@ -176,12 +176,18 @@ constexpr uint32_t kRegularBlock = 256;
 // for two-level plans phase M regroups stage1 by receiver block into stage2; phase B (one
 // receiver block per workgroup) copies its runs into LDS by LDS-DMA, then every lane reads its d
 // values through invpos and applies the rule in registers.
-#ifndef ACS_BIN_SB
-#define ACS_BIN_SB 256
-#endif
-constexpr uint32_t kBinSB = ACS_BIN_SB;   // receivers per phase-B workgroup (one lane each)
+// Receivers per phase-B workgroup (one lane each) is a property of the plan (BinnedPlan::SB), not a
+// build constant: the phase-B grid, invpos layout, tiles and the block-partial slots all follow
+// it (one partial per receiver block, so a handle sizes its partials by the plan's SB).  kBinSB is
+// the default; clean fp64 / fp32 plans of d = 16 / 32 also take 128 (and d = 16 512), by
+// ACSIM_BIN_SB or the per-degree default (binned_block_size).
+constexpr uint32_t kBinSB = 256;
+bool binned_sb_supported(uint32_t d, uint32_t t, uint32_t rule, uint32_t sb, bool clean_fast);
+// the phase-B receiver block a plan of degree d would use (ACSIM_BIN_SB, else the default for d)
+uint32_t binned_block_size(uint32_t d, uint32_t t, uint32_t rule, bool clean_fast);
 struct BinnedPlan {
     uint32_t D = 0, SA = 0, P = 0, Q = 0, levels = 0, PK = 0, ngroups = 0, nrun = 0, mcap = 0;
+    uint32_t SB = kBinSB;               // receivers per phase-B workgroup (receiver block)
     bool f32 = false;                   // fp32 plan (float stage, runs padded to 4 elements)
     uint32_t segs = 0, chunk = 0;       // phase-A workgroups per source block, deliveries per workgroup
     uint64_t E = 0;                     // deliveries = local rows * D
@@ -189,7 +195,7 @@ struct BinnedPlan {
     uint16_t* idxA = nullptr;           // [Ep1] sender index within its source block (0 in pads)
     uint32_t* pkA = nullptr;            // idxA packed to 14 bits (binned_dev.hpp pk14; fp64, SA <= 16384), idxA then freed
     uint16_t* idxM = nullptr;           // [Ep2] position inside the phase-M LDS image (two levels)
-    uint16_t* invpos = nullptr;         // [Q][D/8][kBinSB][8]: position of (receiver, slot) in block b's runs
+    uint16_t* invpos = nullptr;         // [Q][D/8][SB][8]: position of (receiver, slot) in block b's runs
     uint2* tiles = nullptr;             // [Q][nrun+1] (stage start | pad count, element offset in block b's runs)
     bool ofree = false;                 // order-free phase B (rid, no invpos)
     bool var = false;                   // CSR rows below the compiled degree (kEllNone columns)
@@ -211,13 +217,14 @@ struct BinnedPlan {
     uint32_t nfix = 0;
 };
 bool binned_supported(uint32_t d, uint32_t t, uint32_t rule);
-// 1 or 2 exchange levels for NR local receivers of an N-node graph (0: not supported).
-uint32_t binned_levels(uint64_t N, uint64_t NR, uint32_t d, uint32_t sa, uint32_t* sr_out);
+// 1 or 2 exchange levels for NR local receivers of an N-node graph (0: not supported); sb = receiver block.
+uint32_t binned_levels(uint64_t N, uint64_t NR, uint32_t d, uint32_t sa, uint32_t sb, uint32_t* sr_out);
 // Builds the plan from the ELL of the NR local rows (sorted or spec order; slot-dependent configs
-// need spec order); sa = source block size; tagged: the config has a fault schedule; ofree: clean
-// config under a sort-based rule (order-free phase B: rid instead of invpos).
+// need spec order); sa = source block size; sb = receiver block (binned_block_size; must satisfy
+// binned_sb_supported); tagged: the config has a fault schedule; ofree: clean config under a
+// sort-based rule (order-free phase B: rid instead of invpos, sb = kBinSB only).
 hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t NR, uint32_t d, uint32_t dp,
-                        uint32_t sa, bool tagged, bool f32, bool ofree, hipStream_t s, bool var = false,
+                        uint32_t sa, uint32_t sb, bool tagged, bool f32, bool ofree, hipStream_t s, bool var = false,
                         const uint32_t* status = nullptr, bool clean = false);
 void binned_free(BinnedPlan& p);
 // clean: no slot-dependent decision (selects the plain phase-B instantiation)
@@ -229,7 +236,8 @@ struct SrcSel {
     uint32_t n, bpr, bpc, k0;
 };
 // Which phases one launch_round_binned call enqueues: 1 = [tag +] scatter (A), 2 = regroup (M),
-// 4 = gather (B, over a.qlo .. a.qhi).
+// 4 = gather (B, over a.qlo .. a.qhi).  Phase B writes partial slot b of its receiver block b:
+// a.nblk must be at least p.Q (hipErrorInvalidValue otherwise, before anything is launched).
 hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a, bool clean, hipStream_t s,
                                const FinalizeArgs* fin = nullptr, uint32_t phases = 7, SrcSel sel = SrcSel{});
 

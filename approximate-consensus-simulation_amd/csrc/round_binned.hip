@@ -271,17 +271,17 @@ __global__ __launch_bounds__(256) void k_bin_fixup(const uint4* __restrict__ fix
 // dropped and NaN entries into missing ones and applies the receiver's own status — no tag
 // decoding, no Byzantine draws, clean-kernel registers.
 template <int D, int T, bool WMSR = false, bool FAULTY = false, typename VT = double, int NP = 1, bool VAR = false,
-          bool FIX = false>
-__global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) : FIX && NP > 1 && (T || WMSR) ? 4 : 1) void k_bin_gather(const RoundArgs a, const VT* __restrict__ stage,
+          bool FIX = false, int SB = (int)kBinSB>
+__global__ __launch_bounds__(SB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) : FIX && NP > 1 && (T || WMSR) ? 4 : 1) void k_bin_gather(const RoundArgs a, const VT* __restrict__ stage,
                                                        const uint16_t* __restrict__ invpos,
                                                        const uint2* __restrict__ tiles, uint32_t nrun, uint32_t Q,
                                                        uint32_t Qc, uint32_t pol) {
     static_assert(D % 8 == 0, "invpos is read 8 slots at a time");
     static_assert(!(FIX && FAULTY), "FIX replaces the tagged resolution");
     constexpr bool FLT = FAULTY || FIX;   // a fault schedule or loss: receiver status and drop mask
-    // runs are padded to 16-byte multiples; nrun <= D*kBinSB/16 (checked when the plan is built)
+    // runs are padded to 16-byte multiples; nrun <= D*SB/16 (checked when the plan is built)
     __shared__ __attribute__((aligned(16)))
-    VT raw[NP > 1 ? kBinPartCap<D, NP> + 16 / sizeof(VT) : D * kBinSB + D * kBinSB / 16 * (16 / sizeof(VT) - 1)];
+    VT raw[NP > 1 ? kBinPartCap<D, NP, SB> + 16 / sizeof(VT) : D * SB + D * SB / 16 * (16 / sizeof(VT) - 1)];
     InstState* S = a.st;
     if (S->done) return;
     const uint64_t t0 = a.ts ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -294,9 +294,9 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
         if (b < a.nblk && threadIdx.x == 0) a.partial[b] = make_double2(kInf, -kInf);
         return;
     }
-    constexpr uint32_t NW = kBinSB / 64;
+    constexpr uint32_t NW = SB / 64;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t li = (uint64_t)b * kBinSB + threadIdx.x;   // local row
+    const uint64_t li = (uint64_t)b * SB + threadIdx.x;   // local row
     const uint64_t i = a.row0 + li;                              // global receiver
     bool live = li < a.nrows;
     if constexpr (VAR) {   // CSR hub rows (no deliveries in the plan): the generic kernel serves them
@@ -314,7 +314,7 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
     // compare or select per slot and part.
     uint2 pdsc = make_uint2(0u, 0u);
     uint32_t pnxt = 0;
-    constexpr uint32_t cap = kBinPartCap<D, NP>;
+    constexpr uint32_t cap = kBinPartCap<D, NP, SB>;
     const bool clampm = NP == 2 && sizeof(VT) == 8 && !FAULTY && pf && (pol & kPolClampPick);
     uint32_t hi0 = 0;
     const bool adma = clampm && (pol & kPolAsmDma);   // asm saddr LDS-DMA (binned_dev.hpp)
@@ -388,18 +388,18 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
         const uint32_t wd = (t & 6) == 0 ? u.x : (t & 6) == 2 ? u.y : (t & 6) == 4 ? u.z : u.w;
         return (t & 1) ? wd >> 16 : wd & 0xFFFFu;
     };
-    const uint4* ipp = reinterpret_cast<const uint4*>(invpos) + (uint64_t)b * (D / 8) * kBinSB + threadIdx.x;
+    const uint4* ipp = reinterpret_cast<const uint4*>(invpos) + (uint64_t)b * (D / 8) * SB + threadIdx.x;
     if (pol & kPolNtInv) {
         using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
         const u32x4* ipn = reinterpret_cast<const u32x4*>(ipp);
 #pragma unroll
         for (int q = 0; q < D / 8; ++q) {
-            const u32x4 t4 = __builtin_nontemporal_load(ipn + q * kBinSB);
+            const u32x4 t4 = __builtin_nontemporal_load(ipn + q * SB);
             ip[q] = make_uint4(t4.x, t4.y, t4.z, t4.w);
         }
     } else {
 #pragma unroll
-        for (int q = 0; q < D / 8; ++q) ip[q] = ipp[q * kBinSB];
+        for (int q = 0; q < D / 8; ++q) ip[q] = ipp[q * SB];
     }
     VT v[D + 1];
     if constexpr (NP == 1) {
@@ -491,7 +491,7 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
         for (int t = 0; t < D; ++t) {
 #if ACS_DIAG_B == 2   // diagnostic: conflict-free reads that ignore the positions (kept live)
             asm volatile("" ::"v"(pos_of(t)));
-            v[1 + t] = raw[(t * kBinSB + threadIdx.x) % cap];
+            v[1 + t] = raw[(t * SB + threadIdx.x) % cap];
 #else
             const uint32_t q = pos_of(t) + sh0;
             v[1 + t] = raw[q < cap ? q : cap];
@@ -510,7 +510,7 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
 #pragma unroll
         for (int t = 0; t < D; ++t) {
 #if ACS_DIAG_B == 2
-            const VT u = raw[(t * kBinSB + threadIdx.x + 7) % cap];
+            const VT u = raw[(t * SB + threadIdx.x + 7) % cap];
 #else
             const uint32_t q = pos_of(t) - lo1;   // wraps above cap below lo1
             const VT u = raw[q < cap ? q : cap];
@@ -651,7 +651,7 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
         }
         if (pol & kPolSc1X) {   // write-through: no dirty x lines left in L2 at the kernel boundary
             const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-                reinterpret_cast<VT*>(a.xout) + (i - threadIdx.x), 0, (int)(kBinSB * sizeof(VT)), 0x00020000);
+                reinterpret_cast<VT*>(a.xout) + (i - threadIdx.x), 0, (int)(SB * sizeof(VT)), 0x00020000);
             if constexpr (sizeof(VT) == 8) {
                 using UV = unsigned int __attribute__((ext_vector_type(2)));
                 UV bits;
@@ -668,7 +668,7 @@ __global__ __launch_bounds__(kBinSB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMS
             mx = res;
         }
     }
-    block_minmax_store<kBinSB>(mn, mx, a.partial + b, a.eacc);
+    block_minmax_store<SB>(mn, mx, a.partial + b, a.eacc);
     if (a.ts) bin_ts(a.ts, t0, t1);
 }
 
@@ -835,9 +835,10 @@ __global__ __launch_bounds__(kBinSB) void k_bin_gather_of(const RoundArgs a, con
 // rows, or all N); global sender ids j in [0, N).
 //   one level:  key1 = a*Q + b                         (phase B reads stage1)
 //   two levels: key1 = a*R + r, key2 = (r*K + k)*QR + bl  with r = li / SR, k = a / PK,
-//               bl = (li % SR) / kBinSB                (phase B reads stage2)
+//               bl = (li % SR) / SB                    (phase B reads stage2)
 struct BinGeom {
     uint32_t D, dp, SA, P, Q, levels, SR, R, K, PK, QR;
+    uint32_t SB;    // receivers per phase-B block (BinnedPlan::SB)
     uint32_t pad;   // tile lengths padded to 16 bytes: 2 (fp64) or 4 (fp32) elements
     uint32_t none1, none2;   // tile count of level 1 / 2: the key of an absent CSR column (kEllNone),
                              // which sorts past every tile and is skipped by every fill kernel
@@ -859,11 +860,11 @@ __global__ __launch_bounds__(256) void k_bin_keys(const uint32_t* __restrict__ e
     if (col == kEllNone)
         key = level == 1 ? G.none1 : G.none2;
     else if (G.levels == 1)
-        key = a * G.Q + (uint32_t)(li / kBinSB);
+        key = a * G.Q + (uint32_t)(li / G.SB);
     else if (level == 1)
         key = a * G.R + (uint32_t)(li / G.SR);
     else
-        key = ((uint32_t)(li / G.SR) * G.K + a / G.PK) * G.QR + (uint32_t)((li % G.SR) / kBinSB);
+        key = ((uint32_t)(li / G.SR) * G.K + a / G.PK) * G.QR + (uint32_t)((li % G.SR) / G.SB);
     keys[e] = key;
     vals[e] = (uint32_t)e;
 }
@@ -1024,10 +1025,10 @@ __global__ __launch_bounds__(256) void k_bin_inv(uint64_t E, BinGeom G, uint32_t
     if (key >= (G.levels == 1 ? G.none1 : G.none2)) return;
     const uint64_t li = e / G.D;
     const uint32_t t = e % G.D;
-    const uint32_t b = (uint32_t)(li / kBinSB);
+    const uint32_t b = (uint32_t)(li / G.SB);
     const uint32_t j = G.levels == 1 ? key / G.Q : (key / G.QR) % G.K;
     const uint32_t pos = tiles[(uint64_t)b * (nrun + 1) + j].y + (uint32_t)(p - tl[key].x);
-    invpos[(((uint64_t)b * (G.D / 8) + t / 8) * kBinSB + (li % kBinSB)) * 8 + (t & 7)] = (uint16_t)pos;
+    invpos[(((uint64_t)b * (G.D / 8) + t / 8) * G.SB + (li % G.SB)) * 8 + (t & 7)] = (uint16_t)pos;
 }
 
 // rid[b][pos] = receiver (inside block b) of the entry at image position pos (order-free plans)
@@ -1040,10 +1041,10 @@ __global__ __launch_bounds__(256) void k_bin_rid(uint64_t E, BinGeom G, uint32_t
     const uint32_t e = vs[p], key = ks[p];
     if (key >= (G.levels == 1 ? G.none1 : G.none2)) return;
     const uint64_t li = e / G.D;
-    const uint32_t b = (uint32_t)(li / kBinSB);
+    const uint32_t b = (uint32_t)(li / G.SB);
     const uint32_t j = G.levels == 1 ? key / G.Q : (key / G.QR) % G.K;
     const uint32_t pos = tiles[(uint64_t)b * (nrun + 1) + j].y + (uint32_t)(p - tl[key].x);
-    rid[(uint64_t)b * rstride + pos] = (uint8_t)(li % kBinSB);
+    rid[(uint64_t)b * rstride + pos] = (uint8_t)(li % G.SB);
 }
 
 // fix-up list: every sorted position p of the last level whose sender is not honest
@@ -1079,18 +1080,24 @@ bool binned_supported(uint32_t d, uint32_t t, uint32_t rule) {
     return false;
 }
 
-uint32_t binned_levels(uint64_t N, uint64_t NR, uint32_t d, uint32_t sa, uint32_t* sr_out) {
-    if (d == 0 || sa == 0 || NR == 0) return 0;
+uint32_t binned_levels(uint64_t N, uint64_t NR, uint32_t d, uint32_t sa, uint32_t sb, uint32_t* sr_out) {
+    if (d == 0 || sa == 0 || NR == 0 || sb == 0) return 0;
     const uint64_t P = (N + sa - 1) / sa;
-    const uint64_t Q = (NR + kBinSB - 1) / kBinSB;
-    const double run1 = (double)NR * d / ((double)P * (double)Q);
+    const uint64_t Q = (NR + sb - 1) / sb;
+    // (the one- / two-level choice is the default block's, so a plan's level count and its
+    // phase A / M do not change with the receiver block)
+    const uint64_t Q0 = (NR + kBinSB - 1) / kBinSB;
+    const double run1 = (double)NR * d / ((double)P * (double)Q0);
     if (run1 >= 64.0) {
-        if (sr_out) *sr_out = kBinSB;
-        return (uint64_t)P <= (uint64_t)d * kBinSB / 16 ? 1u : 0u;   // phase-B LDS bound
+        if (sr_out) *sr_out = sb;
+        return (uint64_t)P <= (uint64_t)d * sb / 16 && Q >= 1 ? 1u : 0u;   // phase-B LDS bound
     }
     // level-1 runs (a, r) average NR*d / (P * R) with R = NR / SR: about 128 at SR = 128 * P / d
-    uint64_t sr = (128ull * P / d + kBinSB - 1) / kBinSB * kBinSB;
+    // (SR a multiple of both the default block and sb: powers of two)
+    const uint64_t unit = sb > kBinSB ? sb : kBinSB;
+    uint64_t sr = (128ull * P / d + unit - 1) / unit * unit;
     if (sr < 4 * kBinSB) sr = 4 * kBinSB;
+    if (sr % sb) return 0;
     if (sr > 65536) return 0;
     if (sr_out) *sr_out = (uint32_t)sr;
     return 2;
@@ -1195,12 +1202,14 @@ hipError_t tile_sort(const uint32_t* ell, uint64_t E, const BinGeom& G, int leve
 }  // namespace
 
 hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t NR, uint32_t d, uint32_t dp,
-                        uint32_t sa, bool tagged, bool f32, bool ofree, hipStream_t s, bool var,
+                        uint32_t sa, uint32_t sb, bool tagged, bool f32, bool ofree, hipStream_t s, bool var,
                         const uint32_t* status, bool clean) {
     if (var && (f32 || ofree)) return hipErrorNotSupported;   // CSR plans: fp64, invpos phase B
+    // receiver blocks other than kBinSB: clean invpos plans of a compiled (d, sb) pair only
+    if (sb != kBinSB && (var || ofree || tagged || !clean)) return hipErrorInvalidValue;
     hipError_t e = hipSuccess;
     uint32_t sr = 0;
-    const uint32_t levels = binned_levels(N, NR, d, sa, &sr);
+    const uint32_t levels = binned_levels(N, NR, d, sa, sb, &sr);
     if (!levels) return hipErrorNotSupported;
     BinGeom G{};
     G.D = d;
@@ -1208,11 +1217,12 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     G.pad = f32 ? 4u : 2u;
     G.SA = sa;
     G.P = (uint32_t)((N + sa - 1) / sa);
-    G.Q = (uint32_t)((NR + kBinSB - 1) / kBinSB);
+    G.SB = sb;
+    G.Q = (uint32_t)((NR + sb - 1) / sb);
     G.levels = levels;
     G.SR = sr;
     G.R = levels == 1 ? G.Q : (uint32_t)((NR + sr - 1) / sr);
-    G.QR = sr / kBinSB;
+    G.QR = sr / sb;
     G.PK = 1;
     if (levels == 2) {   // chunks of PK source blocks: an LDS image of about 16 Ki deliveries
         const double run1 = (double)NR * d / ((double)G.P * G.R);
@@ -1227,6 +1237,7 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     p.var = var;
     p.D = d;
     p.SA = sa;
+    p.SB = sb;
     p.f32 = f32;
     p.P = G.P;
     p.Q = G.Q;
@@ -1239,7 +1250,7 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     const uint64_t nt1 = (uint64_t)G.P * G.R;
     const uint64_t nt2 = levels == 2 ? (uint64_t)G.R * G.K * G.QR : 0;
     if (E >= (1ull << 32) || nt1 >= (1ull << 32) || nt2 >= (1ull << 32)) return hipErrorNotSupported;
-    if ((uint64_t)p.nrun > (uint64_t)d * kBinSB / 16) return hipErrorNotSupported;   // phase-B LDS bound
+    if ((uint64_t)p.nrun > (uint64_t)d * sb / 16) return hipErrorNotSupported;   // phase-B LDS bound
     const unsigned grid = (unsigned)((E + 255) / 256);
 
     // ---- level 1 (phase A): key (a, b) or (a, r)
@@ -1321,7 +1332,7 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
         last = &T2;
     }
     // ---- phase B tables over the last stage
-    const uint64_t Qp = (uint64_t)G.Q * kBinSB;   // receiver slots incl. the ragged last block's padding
+    const uint64_t Qp = (uint64_t)G.Q * sb;   // receiver slots incl. the ragged last block's padding
     if (e == hipSuccess) e = hipMalloc(&p.tiles, ((uint64_t)p.nrun + 1) * G.Q * sizeof(uint2));
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_bin_prefix, dim3((G.Q + 255) / 256), dim3(256), 0, s, last->pstart, last->plen, last->tl, G,
@@ -1335,7 +1346,7 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
                   : kPolDefault | (G.levels == 2 ? kPolTwoLevelStores : kPolOneLevelStores);
     }
     if (ofree) {   // order-free phase B: receiver ids in image order
-        p.rstride = ((uint32_t)d * kBinSB + p.nrun * (G.pad - 1) + 15u) & ~15u;
+        p.rstride = ((uint32_t)d * sb + p.nrun * (G.pad - 1) + 15u) & ~15u;
         if (e == hipSuccess) e = hipMalloc(&p.rid, (uint64_t)G.Q * p.rstride);
         if (e == hipSuccess) e = hipMemsetAsync(p.rid, 0, (uint64_t)G.Q * p.rstride, s);
         if (e == hipSuccess) {
@@ -1396,7 +1407,7 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
         if (tagged && np > 2) np = 2;          // tagged fp64 phase B: two passes at most
         if (np > 1) {
             const uint32_t D = G.D;
-            const uint32_t cap = D * kBinSB / np + D * kBinSB / 16;   // kBinPartCap<D, np>
+            const uint32_t cap = D * sb / np + D * sb / 16;   // kBinPartCap<D, np, sb>
             std::vector<uint2> h(((uint64_t)p.nrun + 1) * G.Q);
             e = hipMemcpy(h.data(), p.tiles, h.size() * sizeof(uint2), hipMemcpyDeviceToHost);
             bool fits = e == hipSuccess && p.nrun >= np;
@@ -1489,6 +1500,57 @@ static hipError_t binned_set_lds_attributes() {
                                p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                                  \
     }
 
+// ---- receiver blocks other than kBinSB (BinnedPlan::SB): clean plans, t = 5 sort-based rules
+// other than W-MSR, d = 32 at 128 receivers and d = 16 at 128 / 512 (fp64 one or two passes, fp32
+// one pass).  Each (d, SB) is one more phase-B instantiation, so the set stays small.
+bool binned_sb_supported(uint32_t d, uint32_t t, uint32_t rule, uint32_t sb, bool clean_fast) {
+    if (sb == kBinSB) return true;
+    if (!clean_fast || t != 5 || rule == 4 || rule == 0) return false;
+    return (sb == 128 && (d == 16 || d == 32)) || (sb == 512 && d == 16);
+}
+
+uint32_t binned_block_size(uint32_t d, uint32_t t, uint32_t rule, bool clean_fast) {
+    uint32_t sb = kBinSB;
+    if (const char* v = getenv("ACSIM_BIN_SB")) sb = (uint32_t)strtoul(v, nullptr, 10);
+    return binned_sb_supported(d, t, rule, sb, clean_fast) ? sb : kBinSB;
+}
+
+template <int D, int T, typename VT>
+static hipError_t launch_gather_sb(const BinnedPlan& p, const RoundArgs& a, const VT* src, dim3 grid, uint32_t Qc,
+                                   uint32_t pol, hipStream_t s) {
+    if constexpr (T == 5 && (D == 16 || D == 32)) {
+        if (a.rule == 4 || a.rule == 0) return hipErrorNotSupported;
+        const uint32_t np = sizeof(VT) == 8 ? p.split : 1u;   // (fp32: one pass, as at kBinSB)
+#define ACS_SB_LAUNCH(SB_, NP_)                                                                          \
+    hipLaunchKernelGGL((k_bin_gather<D, T, false, false, VT, NP_, false, false, SB_>), grid, dim3(SB_), 0, s, a, \
+                       src, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol)
+        if (p.SB == 128 && np == 1) {
+            ACS_SB_LAUNCH(128, 1);
+            return hipGetLastError();
+        }
+        if constexpr (sizeof(VT) == 8) {
+            if (p.SB == 128 && np == 2) {
+                ACS_SB_LAUNCH(128, 2);
+                return hipGetLastError();
+            }
+        }
+        if constexpr (D == 16) {
+            if (p.SB == 512 && np == 1) {
+                ACS_SB_LAUNCH(512, 1);
+                return hipGetLastError();
+            }
+            if constexpr (sizeof(VT) == 8) {
+                if (p.SB == 512 && np == 2) {
+                    ACS_SB_LAUNCH(512, 2);
+                    return hipGetLastError();
+                }
+            }
+        }
+#undef ACS_SB_LAUNCH
+    }
+    return hipErrorNotSupported;
+}
+
 hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool clean, hipStream_t s,
                                const FinalizeArgs* fin, uint32_t phases, SrcSel sel) {
     const FinalizeArgs fa = fin ? *fin : FinalizeArgs{};
@@ -1500,6 +1562,10 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
     // partials), or the caller's [qlo, qhi)
     RoundArgs a = a0;
     a.ts = p.ts ? p.ts + 3ull * p.ts_a : nullptr;
+    // phase B writes a.partial[b] for each of its receiver blocks b < p.Q (and neutral pairs up to
+    // a.nblk): partials sized for fewer blocks would be written past their slice
+    if ((phases & 4u) && a.nblk < p.Q) return hipErrorInvalidValue;
+    if (p.SB != kBinSB && (!clean || p.var || p.ofree)) return hipErrorInvalidValue;
     const uint32_t nslot_all = a.nblk > p.Q ? a.nblk : p.Q;
     if (a.qhi > nslot_all) a.qhi = nslot_all;
     if (a.qlo >= a.qhi) phases &= ~4u;
@@ -1536,6 +1602,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
         const dim3 grid(8 * Qc);
 #define X(DD, TT)                                                                                        \
     if (p.D == DD && a.trim == TT) {                                                                     \
+        if (p.SB != kBinSB) return launch_gather_sb<DD, TT, float>(p, a, st1, grid, Qc, pol, s);          \
         if (p.ofree && a.rule == 4)                                                                      \
             hipLaunchKernelGGL((k_bin_gather_of<DD, TT, true, float>), grid, dim3(kBinSB), 0, s, a, st1,    \
                                p.rid, p.rstride, p.tiles, p.nrun, p.Q, Qc);                              \
@@ -1601,6 +1668,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
     const dim3 grid(8 * Qc);
 #define X(DD, TT)                                                                                        \
     if (p.D == DD && a.trim == TT) {                                                                     \
+        if (p.SB != kBinSB) return launch_gather_sb<DD, TT, double>(p, a, last, grid, Qc, pol, s);       \
         const bool w_ = a.rule == 4;                                                                     \
         if (p.var && clean && w_)                                                                        \
             hipLaunchKernelGGL((k_bin_gather<DD, TT, true, false, double, 1, true>), grid, dim3(kBinSB), 0, s, \
