@@ -12,6 +12,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/acsim.h"
@@ -705,20 +706,39 @@ static int enqueue_round(acs_sim* s, uint32_t r) {
     return ACS_OK;
 }
 
+// Host memory the device writes and the host polls (run summary, instance states): mapped into the
+// device's address space and explicitly COHERENT, so the device's system-scope release of the
+// sequence number (and the fields stored before it) reaches host memory without a cache flush at
+// the end of the kernel; the polling protocol below depends on that and must not rest on the
+// runtime's default or on HIP_HOST_COHERENT.  acs_runtime_info reports it.
+static constexpr unsigned kPolledHostFlags = hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent;
+
 // Poll a host-mapped sequence number a launch on s->stream releases at system scope.  The stream is
 // queried every 256 spins, so a failed launch returns its error rather than spinning forever.
-static int wait_mapped_seq(acs_sim* s, const unsigned long long* p, unsigned long long seq, const char* what) {
+// patient: the wait may span a whole chunk of long rounds (EPS chunk verdicts of large graphs,
+// milliseconds each): after 100 us of spinning the host sleeps 20 us between polls instead of
+// holding a core (ranks share the box's cores; the extra wake-up latency is well under 1 % of such a
+// chunk).  The short call-end reads spin throughout (their wait is a few microseconds).
+static int wait_mapped_seq(acs_sim* s, const unsigned long long* p, unsigned long long seq, const char* what,
+                           bool patient = false) {
+    const auto t0 = std::chrono::steady_clock::now();
+    bool sleeping = false;
     for (uint32_t it = 1;; ++it) {
         if (__atomic_load_n(p, __ATOMIC_ACQUIRE) == seq) return ACS_OK;
-        if ((it & 255u) == 0) {
+        if (sleeping || (it & 255u) == 0) {
             const hipError_t q = hipStreamQuery(s->stream);
             if (q == hipSuccess) {
                 if (__atomic_load_n(p, __ATOMIC_ACQUIRE) == seq) return ACS_OK;
                 return fail(ACS_EDEVICE, "%s: stream idle without the sequence number", what);
             }
             if (q != hipErrorNotReady) return fail(ACS_EDEVICE, "%s: %s", what, hipGetErrorString(q));
+            if (patient && !sleeping && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(100))
+                sleeping = true;
         }
-        __builtin_ia32_pause();
+        if (sleeping)
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+        else
+            __builtin_ia32_pause();
     }
 }
 
@@ -726,17 +746,18 @@ static int wait_mapped_seq(acs_sim* s, const unsigned long long* p, unsigned lon
 // instances take them through host-mapped memory (launch_states_mapped: no device-to-host copy,
 // no wait on the stream's completion signal); the stream may still be retiring that small launch
 // on return, and later work stays ordered behind it.
-static int fetch_mapped_states(acs_sim* s) {
+static int fetch_mapped_states(acs_sim* s, bool patient = false) {
     const unsigned long long seq = ++s->ms_seq;
     HIP_TRY(launch_states_mapped(s->st, s->n_done, (uint32_t)s->B, s->h_ms_dev, seq, s->stream));
-    return wait_mapped_seq(s, &s->h_ms->seq, seq, "instance states");
+    return wait_mapped_seq(s, &s->h_ms->seq, seq, "instance states", patient);
 }
 
 // The done count after everything enqueued so far (EPS chunks and call ends): through the mapped
-// states where the handle has them (which then hold the states of that moment too).
-static int fetch_done_count(acs_sim* s, uint32_t& nd) {
+// states where the handle has them (which then hold the states of that moment too).  patient: a
+// chunk verdict behind a chunk of long rounds (wait_mapped_seq).
+static int fetch_done_count(acs_sim* s, uint32_t& nd, bool patient = false) {
     if (s->h_ms) {
-        if (int rc = fetch_mapped_states(s)) return rc;
+        if (int rc = fetch_mapped_states(s, patient)) return rc;
         nd = s->h_ms->n_done;
         return ACS_OK;
     }
@@ -861,7 +882,7 @@ static int advance(acs_sim* s, uint32_t k) {
         if (s->round >= s->c.max_rounds) break;
         if (sync_poll && k > 0) {
             uint32_t nd = 0;
-            if (int rc = fetch_done_count(s, nd)) return rc;
+            if (int rc = fetch_done_count(s, nd, true)) return rc;
             if (nd == s->B) s->all_done = true;
         } else if (eps_mode && !sync_poll) {
             // keep one chunk in flight: poll the previous chunk's done counter
@@ -1166,11 +1187,11 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     }
     CREATE_TRY(hipMalloc(&s->n_done, sizeof(uint32_t)));
     CREATE_TRY(hipHostMalloc(&s->h_ndone, 2 * sizeof(uint32_t), hipHostMallocDefault));
-    CREATE_TRY(hipHostMalloc(&s->h_sum, sizeof(RunSummary), hipHostMallocMapped | hipHostMallocPortable));
+    CREATE_TRY(hipHostMalloc(&s->h_sum, sizeof(RunSummary), kPolledHostFlags));
     CREATE_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&s->h_sum_dev), s->h_sum, 0));
     memset(s->h_sum, 0, sizeof(RunSummary));
     if (s->B <= kMappedStates) {
-        CREATE_TRY(hipHostMalloc(&s->h_ms, sizeof(MappedStates), hipHostMallocMapped | hipHostMallocPortable));
+        CREATE_TRY(hipHostMalloc(&s->h_ms, sizeof(MappedStates), kPolledHostFlags));
         CREATE_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&s->h_ms_dev), s->h_ms, 0));
         memset(s->h_ms, 0, sizeof(MappedStates));
     }
@@ -1418,7 +1439,7 @@ int acs_runtime_info(char* out, uint64_t cap) {
     int hv = 0, nv = 0;
     if (hipRuntimeGetVersion(&hv) != hipSuccess) return fail(ACS_EDEVICE, "hipRuntimeGetVersion failed");
     if (ncclGetVersion(&nv) != ncclSuccess) return fail(ACS_ECOMM, "ncclGetVersion failed");
-    snprintf(out, cap, "hip %d rccl %d", hv, nv);
+    snprintf(out, cap, "hip %d rccl %d polled-host-flags 0x%x", hv, nv, kPolledHostFlags);
     return ACS_OK;
 }
 

@@ -245,8 +245,16 @@ __device__ __forceinline__ void bin_stream_pk14_t(const VT* lx, const uint32_t* 
             const uint32_t nh = __builtin_nontemporal_load(pk16 + mn * (2 * kPk14Words) + 384 + lane);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
+#if defined(ACS_DIAG_A) && ACS_DIAG_A == 1
+                // diagnostic (variant builds only, wrong values): the same extracts, kept live, but
+                // bank-conflict-free LDS reads (consecutive 8-byte words across the wave)
+                const uint32_t x0 = pk14_extract(c0, c1, c2, ch, 2 * q), x1 = pk14_extract(c0, c1, c2, ch, 2 * q + 1);
+                asm volatile("" ::"v"(x0), "v"(x1));
+                const V2 v = bin_pair(lx[(q * 128u + lane) & 16383u], lx[(q * 128u + 64u + lane) & 16383u]);
+#else
                 const V2 v = bin_pair(lx[pk14_extract(c0, c1, c2, ch, 2 * q)],
                                       lx[pk14_extract(c0, c1, c2, ch, 2 * q + 1)]);
+#endif
                 const uint64_t vi = m * 256 + q * 64 + lane;   // pair index of positions 2vi, 2vi + 1
                 if constexpr (SMODE == 2) {
                     // (buffer offsets are 32-bit: the descriptor is re-based per 1 GiB of stage)

@@ -37,7 +37,8 @@
 #include <vector>
 
 // ACS_DIAG_B (variant builds only, tools/build_variant.sh; wrong values): the clean two-pass phase B
-// without 1 its selection network, 2 its position-dependent pick-up, 3 its stage DMA
+// without 1 its selection network, 2 its position-dependent pick-up, 3 its stage DMA, 4 its invpos
+// stream (in-range synthetic positions)
 #ifndef ACS_DIAG_B
 #define ACS_DIAG_B 0
 #endif
@@ -389,6 +390,18 @@ __global__ __launch_bounds__(SB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) :
         return (t & 1) ? wd >> 16 : wd & 0xFFFFu;
     };
     const uint4* ipp = reinterpret_cast<const uint4*>(invpos) + (uint64_t)b * (D / 8) * SB + threadIdx.x;
+#if ACS_DIAG_B == 4   // diagnostic: no invpos stream; in-range synthetic positions (wrong values)
+    if (true) {
+#pragma unroll
+        for (int q = 0; q < D / 8; ++q) {
+            uint32_t w4[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                w4[e] = ((8 * q + 2 * e) * SB + threadIdx.x) | ((8 * q + 2 * e + 1) * SB + threadIdx.x) << 16;
+            ip[q] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        }
+    } else
+#endif
     if (pol & kPolNtInv) {
         using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
         const u32x4* ipn = reinterpret_cast<const u32x4*>(ipp);

@@ -279,6 +279,7 @@ def leg_cfg3(ctx: Ctx, reps: int = 8) -> dict:
     off, cnt = shard_range(cfg.n_instances, ctx.world, ctx.rank)
     local = cfg.replace(n_instances=max(cnt, 1), instance_offset=off)
     sims = []
+    one = None
     err = None
     try:
         with acsim.Simulator(local.replace(n_instances=min(256, max(cnt, 1))), device=ctx.dev) as w:
@@ -290,6 +291,13 @@ def leg_cfg3(ctx: Ctx, reps: int = 8) -> dict:
     except Exception as e:  # noqa: BLE001
         err = f"{type(e).__name__}: {e}"
     if not ctx.all_ok(err is None):
+        # release whatever this rank did create before raising (its device buffers would stay
+        # allocated while the remaining legs run)
+        for sim in ([one] if one is not None else []) + sims:
+            try:
+                sim.close()
+            except Exception:  # noqa: BLE001
+                pass
         raise RuntimeError(err or "another rank failed to create its cfg3 shard")
     ctx.barrier(one)
     t0 = time.perf_counter()

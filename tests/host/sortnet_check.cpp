@@ -1,7 +1,7 @@
 // Host check of csrc/sortnet.hpp (compiled with g++ by tests/test_sortnet_host.py):
 //  1. every selection network the register kernels instantiate (M = d + 1 entries, window [t, M - t))
 //     puts the window's order statistics where std::sort does, on random multisets with ties, and
-//     passes the 0-1 principle (exhaustively up to 17 entries, sampled at 33);
+//     passes the 0-1 principle (exhaustively: every 0-1 vector, 2^33 at d = 32);
 //  2. the NZ tree sum (padding adds skipped, one final +0.0) equals the spec's tree bit for bit,
 //     signed zeros and denormals included.
 #include <algorithm>
@@ -78,6 +78,48 @@ static long check_01(std::mt19937_64& g, long samples) {
     return bad;
 }
 
+// 0-1 principle, EXHAUSTIVE for any M <= 40 (the 33-entry networks were only sampled):
+// the low 6 wires carry the lane index (64 inputs per word) and the other M - 6 wires are constant
+// in a word (all ones or all zeros, from the word index w), so an input's count of ones is
+// popcount(lane) + popcount(w) and the sorted value of window position k is one exactly for the
+// lanes with popcount(lane) >= M - k - popcount(w): one precomputed lane mask per threshold.
+// 2^(M-6) words (2^27 at M = 33), split over OpenMP threads.
+template <int M, int LO, int HI>
+static long check_01_all() {
+    static_assert(M > 6 && M <= 40, "lanes carry 6 wires");
+    using Net = SelectNet<M, LO, HI>;
+    uint64_t lanes[6], ge[8];   // ge[t]: lanes with popcount >= t (t = 0..7)
+    for (int k = 0; k < 6; ++k) {
+        lanes[k] = 0;
+        for (int j = 0; j < 64; ++j) lanes[k] |= (uint64_t)((j >> k) & 1) << j;
+    }
+    for (int t = 0; t < 8; ++t) {
+        ge[t] = 0;
+        for (int j = 0; j < 64; ++j) ge[t] |= (uint64_t)(__builtin_popcount(j) >= t) << j;
+    }
+    const long words = 1L << (M - 6);
+    long bad = 0;
+#pragma omp parallel for schedule(static) reduction(+ : bad)
+    for (long w = 0; w < words; ++w) {
+        uint64_t x[M];
+        for (int k = 0; k < 6; ++k) x[k] = lanes[k];
+        for (int k = 6; k < M; ++k) x[k] = ((w >> (k - 6)) & 1) ? ~0ull : 0ull;
+        const int pw = __builtin_popcountl((unsigned long)w);
+        for (int q = 0; q < Net::count; ++q) {
+            const int a = Net::list.c[q].a, b = Net::list.c[q].b;
+            const uint64_t lo = x[a] & x[b], hi = x[a] | x[b];
+            x[a] = lo;
+            x[b] = hi;
+        }
+        for (int k = LO; k < HI; ++k) {
+            const int t = M - k - pw;   // lanes whose popcount reaches t hold a one at rank k
+            const uint64_t want = t <= 0 ? ~0ull : t > 6 ? 0ull : ge[t];
+            bad += __builtin_popcountll(x[Net::net.perm[k]] ^ want);
+        }
+    }
+    return bad;
+}
+
 template <int N, int OFF, int STRIDE, int M>
 static long check_tree(const double (&a)[M]) {
     return bits(tree_sum_const<N, OFF, STRIDE, false>(a)) != bits(tree_sum_const<N, OFF, STRIDE, true>(a));
@@ -97,6 +139,9 @@ int main() {
     bad += check_01<9, 2, 7>(g, 0);
     bad += check_01<33, 5, 28>(g, 60000);     // 3.8 M random 0-1 vectors, all densities
     bad += check_01<33, 0, 33>(g, 60000);
+    bad += check_01_all<33, 5, 28>();          // every one of the 2^33 0-1 vectors (cfg4's network)
+    bad += check_01_all<33, 0, 33>();
+    bad += check_01_all<17, 5, 12>();          // (the same checker on the exhaustively checked 17)
     long nbad_net = bad;
     const double pool[] = {0.0, -0.0, 5e-324, -5e-324, 1.0, -1.0, 0.5, -0.5, 1e-310, -1e-310, 3.0, -3.0};
     long ntree = 0;

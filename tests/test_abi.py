@@ -138,6 +138,14 @@ def test_runtime_info_reports_the_rocm_libraries(acsim_lib):
     process mapped for them — bench.py records them per rank so an N > 1 run can be checked to
     run on the same libraries as the single-GPU run and the GPU suite."""
     info = _abi.runtime_info()
-    assert re.fullmatch(r"hip \d+ rccl \d+", info["versions"]), info
+    m = re.fullmatch(r"hip \d+ rccl \d+ polled-host-flags 0x([0-9a-f]+)", info["versions"])
+    assert m, info
+    # the host memory the round loop polls (run summary, instance states) is mapped, and requests
+    # coherence explicitly (hipHostMallocCoherent 0x40000000, never NonCoherent 0x80000000), so
+    # the sequence-number protocol does not rest on the runtime's default (VERDICT r05 item 4)
+    flags = int(m.group(1), 16)
+    assert flags & 0x2, hex(flags)                    # hipHostMallocMapped
+    assert flags & 0x40000000, hex(flags)             # hipHostMallocCoherent
+    assert not flags & 0x80000000, hex(flags)
     assert len(info["libamdhip64"]) == 1 and info["libamdhip64"][0].startswith("/opt/rocm"), info
     assert len(info["librccl"]) == 1 and info["librccl"][0].startswith("/opt/rocm"), info

@@ -14,7 +14,7 @@ CSRC = os.path.join(os.path.dirname(HERE), "approximate-consensus-simulation_amd
 @pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
 def test_sortnet_and_nz_tree_on_host(tmp_path):
     exe = tmp_path / "sortnet_check"
-    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", CSRC,
+    subprocess.run(["g++", "-O2", "-fopenmp", "-std=c++17", "-ffp-contract=off", "-I", CSRC,
                     os.path.join(HERE, "host", "sortnet_check.cpp"), "-o", str(exe)], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
