@@ -1095,17 +1095,13 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
     uint32_t bin_sa = 16384u;
     if (const char* v = getenv("ACSIM_BIN_SA")) bin_sa = (uint32_t)strtoul(v, nullptr, 10);
     if (bin_sa < 64 || bin_sa > sa_max || (bin_sa & (bin_sa - 1))) bin_sa = 16384u;
-    // order-free phase B (clean, sort-based rule: the rows are stored sorted and the rule sees a
-    // multiset), ACSIM_BIN_OF=1: measured slower than the invpos phase B, kept as
-    // a tested variant
+    // (the order-free phase B of rounds 1-5, ACSIM_BIN_OF=1, measured slower than the invpos phase
+    // B and was removed in round 6: DESIGN.md §5.1, §5.13)
     std::string kname_lane;   // (set with the binned decision below)
-    const char* of_env = getenv("ACSIM_BIN_OF");
-    // (rid is one byte per entry: receiver blocks of kBinSB = 256)
-    const bool bin_of = s->ell_sorted && of_env && of_env[0] == '1' && !s->csr_var;
     // phase-B receiver block (BinnedPlan::SB): the default, or ACSIM_BIN_SB where the clean (d, t)
     // pair has that instantiation; block partials follow it (one per receiver block)
     const uint32_t bin_sb = binned_block_size(s->d, cfg->trim, cfg->rule,
-                                              s->clean && !s->csr_var && !bin_of && s->path == PATH_REGULAR);
+                                              s->clean && !s->csr_var && s->path == PATH_REGULAR);
     {
         const char* env = getenv("ACSIM_BINNED");
         const bool allow = !(env && env[0] == '0');
@@ -1248,8 +1244,8 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         bool bin_refused = false;
         auto try_plan = [&](BinnedPlan& plan, const uint32_t* ell, uint64_t nr) -> hipError_t {
             if (!s->binned || bin_refused || !nr) return hipSuccess;
-            hipError_t e = binned_build(plan, ell, s->N, nr, s->d, s->dp, bin_sa, bin_sb, tagged, s->f32, bin_of,
-                                        s->stream, false, s->status, s->clean);
+            hipError_t e = binned_build(plan, ell, s->N, nr, s->d, s->dp, bin_sa, bin_sb, tagged, s->f32, s->stream,
+                                        false, s->status, s->clean);
             if (e == hipErrorNotSupported) {
                 bin_refused = true;
                 return hipSuccess;
@@ -1281,7 +1277,6 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
             // NP-pass phase B (slot-dependent configs: fp64, two passes only; see launch_round_binned)
             if (s->bin.split > 1 && (s->clean || (!s->f32 && s->bin.split == 2)))
                 s->kname += " split" + std::to_string(s->bin.split);
-            if (s->bin.ofree) s->kname += " orderfree";
             if (s->bin.pkA)   // 14-bit packed phase-A index stream
                 s->kname += " pk14A";
             if (s->bin.fix) {   // fault fix-up list instead of tagged senders
@@ -1301,7 +1296,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         CREATE_TRY(hipMalloc(&s->colidx, (csr_nnz ? csr_nnz : 1) * sizeof(uint32_t)));
         CREATE_TRY(hipMemcpy(s->rowptr, h_rowptr, (s->N + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
         if (csr_nnz) CREATE_TRY(hipMemcpy(s->colidx, h_colidx, csr_nnz * sizeof(uint32_t), hipMemcpyHostToDevice));
-        if (s->csr_var) {   // padded ELL (SELL-64 slice widths), sorted rows when order-free, binned plan
+        if (s->csr_var) {   // padded ELL (SELL-64 slice widths), sorted rows when order-independent, binned plan
             const uint64_t words = ((s->N + 63) / 64) * 64ull * s->dp;
             CREATE_TRY(hipMalloc(&s->ell, words * sizeof(uint32_t)));
             CREATE_TRY(hipMalloc(&s->deg, s->N));
@@ -1311,7 +1306,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
             if (s->ell_sorted) CREATE_TRY(launch_sort_ell_rows(s->ell, s->N, s->d, s->stream));
             if (s->binned) {
                 const hipError_t be = binned_build(s->bin, s->ell, s->N, s->N, s->d, s->dp, bin_sa, kBinSB, tagged,
-                                                   s->f32, false, s->stream, true, s->status);
+                                                   s->f32, s->stream, true, s->status);
                 if (be == hipErrorNotSupported) {   // the plan does not fit: the per-lane kernel serves the rows
                     binned_free(s->bin);
                     s->binned = false;

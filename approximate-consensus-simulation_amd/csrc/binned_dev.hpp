@@ -11,12 +11,11 @@ namespace acs {
 constexpr uint32_t kBinA = 512;        // phase-A / phase-M workgroup: 8 waves
 constexpr uint32_t kBinMCap = 19456;   // phase-M LDS image capacity (elements, 152 KiB)
 // cache-policy switches of the exchange (launch argument `pol`; ACSIM_BIN_POL overrides the default)
-constexpr uint32_t kPolNtRuns = 1;     // phase B: stage runs by nontemporal LDS-DMA
-constexpr uint32_t kPolNtStore = 2;    // phase A: nontemporal stage stores
-constexpr uint32_t kPolNtInv = 4;      // phase B: nontemporal invpos loads
-constexpr uint32_t kPolRevB = 8;       // phase B: each XCD walks its receiver-block range downwards
-                                       // (the stage tiles phase A wrote last are read first)
-constexpr uint32_t kPolNoPf = 16;       // phase B (NP > 1): per-part descriptor loads instead of the prefetch
+// (Retired in round 6, measured slower in the driver's shape and in 200-round A/Bs, DESIGN.md §5.11;
+// their bits are ignored now: 1 nontemporal phase-B run copies, 4 plain instead of nontemporal
+// invpos loads — the nontemporal load is unconditional —, 8 RevB (each XCD walking its receiver
+// blocks downwards), 16 NoPf (per-part descriptor loads instead of the prefetch).  In git history.)
+constexpr uint32_t kPolNtStore = 2;    // phase A: nontemporal stage stores (two-level plans' default)
 constexpr uint32_t kPolBfPick = 32;     // phase B (NP > 1): branch-free pick-up (clamped read + select)
 constexpr uint32_t kPolSc1Store = 64;   // phase A: write-through (sc1) stage stores instead of nt: no
                                         // dirty stage lines left in L2 for the kernel boundary to write back
@@ -41,7 +40,7 @@ constexpr uint32_t kPolMask = 32767;     // every switch (ACSIM_BIN_POL)
 // 7.60 against 7.86 ms per round for plain ones (the 16 GiB of stages far exceed the MALL)
 constexpr uint32_t kPolOneLevelStores = kPolSc1Store;
 constexpr uint32_t kPolTwoLevelStores = kPolNtStore | kPolNtStoreM;
-constexpr uint32_t kPolDefault = kPolNtInv | kPolBfPick | kPolClampPick | kPolBytePick | kPolAsmDma | kPolAsmDmaT;
+constexpr uint32_t kPolDefault = kPolBfPick | kPolClampPick | kPolBytePick | kPolAsmDma | kPolAsmDmaT;
 // measured (cfg4): phase B 80 -> 71 (nt invpos) -> 63.2 us (pick-up); the clamped pick-up: round 117.2-118.8 ->
 // 112.3-112.9 us; the packed 16-bit pick-up: 112.2-113.0 -> 110.2-111.0 us; the asm run copies:
 // a further -0.4 us, and cfg4 fp32 (one-pass phase B) 79.0 -> 76.8 us (§5.11)
@@ -297,7 +296,7 @@ __device__ __forceinline__ void bin_stream_pk14(const VT* lx, const uint32_t* __
 // Runs are padded to EPU = 16 / sizeof(VT) elements (2 for fp64, 4 for fp32).
 template <typename VT = double>
 __device__ __forceinline__ void bin_dma_runs(const uint2* __restrict__ tb, uint32_t r0, uint32_t r1,
-                                             const VT* __restrict__ src, VT* dst, bool nt = false,
+                                             const VT* __restrict__ src, VT* dst,
                                              uint32_t base = 0) {   // base: image offset of dst[0]
     constexpr uint32_t EPU = 16 / sizeof(VT);
     const uint32_t lane = threadIdx.x & 63;
@@ -317,13 +316,8 @@ __device__ __forceinline__ void bin_dma_runs(const uint2* __restrict__ tb, uint3
             const uint32_t n16 = (__builtin_amdgcn_readlane(nxt, k) - pre) / EPU;   // 16-byte units
             const uint4* sp = s16 + so / EPU + lane;
             uint4* dp = d16 + (pre - base) / EPU;
-            if (nt) {   // once-read runs: nontemporal policy (aux = 2)
-                for (uint32_t o = 0; o < n16; o += 64)
-                    if (o + lane < n16) __builtin_amdgcn_global_load_lds(sp + o, dp + o, 16, 0, 2);
-            } else {
-                for (uint32_t o = 0; o < n16; o += 64)
-                    if (o + lane < n16) __builtin_amdgcn_global_load_lds(sp + o, dp + o, 16, 0, 0);
-            }
+            for (uint32_t o = 0; o < n16; o += 64)
+                if (o + lane < n16) __builtin_amdgcn_global_load_lds(sp + o, dp + o, 16, 0, 0);
         }
     }
 }
@@ -358,18 +352,12 @@ __device__ __forceinline__ void bin_dma_runs_pf(uint2 dsc, uint32_t nxt, uint32_
 // restores it after the issue: whatever M0 value the compiler's own LDS-DMA or M0-indexed code
 // holds across the statement is preserved by construction.  (The instruction reads M0 at issue,
 // so rewriting it right after is safe: consecutive copies already rewrite it back to back.)
-template <bool NT>
 __device__ __forceinline__ void bin_lds_dma16(uint32_t voff, uint64_t sbase, uint32_t m0) {
 #if defined(__HIP_DEVICE_COMPILE__)
     uint32_t saved;
-    if constexpr (NT)
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt\n\t"
-                     "s_mov_b32 m0, %0"
-                     : "=&s"(saved) : "v"(voff), "s"(sbase), "s"(m0) : "memory");
-    else
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
-                     "s_mov_b32 m0, %0"
-                     : "=&s"(saved) : "v"(voff), "s"(sbase), "s"(m0) : "memory");
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(saved) : "v"(voff), "s"(sbase), "s"(m0) : "memory");
 #endif
 }
 
@@ -393,14 +381,14 @@ __device__ __forceinline__ void bin_dma_runs_asm(uint32_t so_l, uint32_t pk_l, u
         const uint64_t sb = (uint64_t)(uintptr_t)src + (uint64_t)(so & ~(16u / sizeof(VT) - 1u)) * sizeof(VT);
         const uint32_t m0 = lb + (pre - base) * (uint32_t)sizeof(VT);
         for (uint32_t o = 0; o < n16; o += 64)
-            if (lane < n16 - o) bin_lds_dma16<false>(voff, sb + o * 16u, m0 + o * 16u);
+            if (lane < n16 - o) bin_lds_dma16(voff, sb + o * 16u, m0 + o * 16u);
     }
 #endif
 }
 // bin_dma_runs with asm copies (kPolAsmDmaT): descriptors fetched one per lane, 64 at a time, as
 // there; each run's stage address in an SGPR pair and its LDS destination in M0 (bin_dma_runs_asm).
 // The caller waits with bin_dma_wait before the barrier that publishes the image.
-template <bool NT, typename VT = double>
+template <typename VT = double>
 __device__ __forceinline__ void bin_dma_runs_asm_tb(const uint2* __restrict__ tb, uint32_t r0, uint32_t r1,
                                                     const VT* __restrict__ src, VT* dst, uint32_t base = 0) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -425,7 +413,7 @@ __device__ __forceinline__ void bin_dma_runs_asm_tb(const uint2* __restrict__ tb
             const uint64_t sb = (uint64_t)(uintptr_t)src + (uint64_t)so * sizeof(VT);
             const uint32_t m0 = lb + (pre - base) * (uint32_t)sizeof(VT);
             for (uint32_t o = 0; o < n16; o += 64)
-                if (lane < n16 - o) bin_lds_dma16<NT>(voff, sb + o * 16u, m0 + o * 16u);
+                if (lane < n16 - o) bin_lds_dma16(voff, sb + o * 16u, m0 + o * 16u);
         }
     }
 #endif

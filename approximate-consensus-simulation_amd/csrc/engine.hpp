@@ -197,12 +197,9 @@ struct BinnedPlan {
     uint16_t* idxM = nullptr;           // [Ep2] position inside the phase-M LDS image (two levels)
     uint16_t* invpos = nullptr;         // [Q][D/8][SB][8]: position of (receiver, slot) in block b's runs
     uint2* tiles = nullptr;             // [Q][nrun+1] (stage start | pad count, element offset in block b's runs)
-    bool ofree = false;                 // order-free phase B (rid, no invpos)
     bool var = false;                   // CSR rows below the compiled degree (kEllNone columns)
     uint32_t split = 1;                 // phase-B passes over the image (ACSIM_BIN_SPLIT; 1 = whole image)
     uint32_t pol = 0;                   // cache-policy switches (round_binned.hip kPol*)
-    uint32_t rstride = 0;               // bytes per receiver block in rid
-    uint8_t* rid = nullptr;             // [Q][rstride] receiver inside block b of each image position (ofree)
     uint2* mt = nullptr;                // [ngroups][PK+1] phase-M run tables (two levels)
     uint64_t* aoff = nullptr;           // [P+1] stage1 start of source block a
     uint64_t* moff = nullptr;           // [ngroups+1] stage2 start of phase-M group g
@@ -221,10 +218,9 @@ bool binned_supported(uint32_t d, uint32_t t, uint32_t rule);
 uint32_t binned_levels(uint64_t N, uint64_t NR, uint32_t d, uint32_t sa, uint32_t sb, uint32_t* sr_out);
 // Builds the plan from the ELL of the NR local rows (sorted or spec order; slot-dependent configs
 // need spec order); sa = source block size; sb = receiver block (binned_block_size; must satisfy
-// binned_sb_supported); tagged: the config has a fault schedule; ofree: clean config under a
-// sort-based rule (order-free phase B: rid instead of invpos, sb = kBinSB only).
+// binned_sb_supported); tagged: the config has a fault schedule.
 hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t NR, uint32_t d, uint32_t dp,
-                        uint32_t sa, uint32_t sb, bool tagged, bool f32, bool ofree, hipStream_t s, bool var = false,
+                        uint32_t sa, uint32_t sb, bool tagged, bool f32, hipStream_t s, bool var = false,
                         const uint32_t* status = nullptr, bool clean = false);
 void binned_free(BinnedPlan& p);
 // clean: no slot-dependent decision (selects the plain phase-B instantiation)

@@ -180,7 +180,7 @@ __global__ __launch_bounds__(kBinA) void k_bin_regroup(const VT* __restrict__ st
     constexpr uint32_t NW = kBinA / 64;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (pol & kPolAsmDmaT) {
-        bin_dma_runs_asm_tb<false>(mt + (uint64_t)g * (PK + 1), w * PK / NW, (w + 1) * PK / NW, stage1, lm);
+        bin_dma_runs_asm_tb(mt + (uint64_t)g * (PK + 1), w * PK / NW, (w + 1) * PK / NW, stage1, lm);
         bin_dma_wait();
     } else {
         bin_dma_runs(mt + (uint64_t)g * (PK + 1), w * PK / NW, (w + 1) * PK / NW, stage1, lm);
@@ -289,7 +289,7 @@ __global__ __launch_bounds__(SB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) :
     uint64_t t1 = 0;
     // XCD-aware order: consecutive receiver blocks (which share the lines at their tile-run
     // seams) run on the same XCD (dispatch is round-robin over the 8 XCDs by blockIdx)
-    const uint32_t b = a.qlo + (blockIdx.x & 7u) * Qc + ((pol & kPolRevB) ? Qc - 1 - (blockIdx.x >> 3) : (blockIdx.x >> 3));
+    const uint32_t b = a.qlo + (blockIdx.x & 7u) * Qc + (blockIdx.x >> 3);
     if (b >= a.qhi) return;   // past this launch's block range
     if (b >= Q) {   // partial slots past this partition's blocks: neutral (the finalize folds a.nblk)
         if (b < a.nblk && threadIdx.x == 0) a.partial[b] = make_double2(kInf, -kInf);
@@ -307,7 +307,7 @@ __global__ __launch_bounds__(SB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) :
     // NP-pass blocks of at most 64 runs: every wave fetches all descriptors first (one per lane)
     // and issues part 0's DMA before anything else is in flight, so the only wait ahead of the
     // first transfer is the descriptor load itself; later parts issue from registers.
-    const bool pf = NP > 1 && nrun <= 64 && !(pol & kPolNoPf);
+    const bool pf = NP > 1 && nrun <= 64;
     // Clamped pick-up (kPolClampPick; two passes, prefetched descriptors, not the tagged kernels):
     // part 0 lies END-aligned in the buffer (image position p at raw[p + cap - hi0]) and part 1
     // start-aligned (p at raw[p - lo1]); raw[cap] holds zeros.  A slot's index, clamped to cap, then
@@ -402,7 +402,7 @@ __global__ __launch_bounds__(SB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) :
         }
     } else
 #endif
-    if (pol & kPolNtInv) {
+    {   // once-read stream: nontemporal loads (phase B 80 -> 71 us on cfg4)
         using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
         const u32x4* ipn = reinterpret_cast<const u32x4*>(ipp);
 #pragma unroll
@@ -410,20 +410,14 @@ __global__ __launch_bounds__(SB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) :
             const u32x4 t4 = __builtin_nontemporal_load(ipn + q * SB);
             ip[q] = make_uint4(t4.x, t4.y, t4.z, t4.w);
         }
-    } else {
-#pragma unroll
-        for (int q = 0; q < D / 8; ++q) ip[q] = ipp[q * SB];
     }
     VT v[D + 1];
     if constexpr (NP == 1) {
         if (pol & kPolAsmDmaT) {
-            if (pol & kPolNtRuns)
-                bin_dma_runs_asm_tb<true>(tb, w * nrun / NW, (w + 1) * nrun / NW, stage, raw);
-            else
-                bin_dma_runs_asm_tb<false>(tb, w * nrun / NW, (w + 1) * nrun / NW, stage, raw);
+            bin_dma_runs_asm_tb(tb, w * nrun / NW, (w + 1) * nrun / NW, stage, raw);
             bin_dma_wait();
         } else {
-            bin_dma_runs(tb, w * nrun / NW, (w + 1) * nrun / NW, stage, raw, (pol & kPolNtRuns) != 0);
+            bin_dma_runs(tb, w * nrun / NW, (w + 1) * nrun / NW, stage, raw);
         }
         __syncthreads();
         if (a.ts) t1 = __builtin_amdgcn_s_memrealtime();
@@ -551,8 +545,7 @@ __global__ __launch_bounds__(SB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) :
             if (pf) {
                 if (k) bin_dma_runs_pf(pdsc, pnxt, j0 + w * (j1 - j0) / NW, j0 + (w + 1) * (j1 - j0) / NW, stage, raw, lo);
             } else {
-                bin_dma_runs(tb, j0 + w * (j1 - j0) / NW, j0 + (w + 1) * (j1 - j0) / NW, stage, raw,
-                             (pol & kPolNtRuns) != 0, lo);
+                bin_dma_runs(tb, j0 + w * (j1 - j0) / NW, j0 + (w + 1) * (j1 - j0) / NW, stage, raw, lo);
             }
             __syncthreads();
             if (k == 0 && a.ts) t1 = __builtin_amdgcn_s_memrealtime();
@@ -683,164 +676,6 @@ __global__ __launch_bounds__(SB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) :
     }
     block_minmax_store<SB>(mn, mx, a.partial + b, a.eacc);
     if (a.ts) bin_ts(a.ts, t0, t1);
-}
-
-// ------------------------------------------------------------------------------ phase B, order-free
-// Clean configs under the sort-based rules (TRIMMED / MIDPOINT / DLPSW / W-MSR) hand the rule a
-// multiset: the slot order of a receiver's values is free.  Phase B then needs no (receiver, slot)
-// position table.  rid[b][image position] (u8: 1 B per delivery instead of invpos's 2 B) names the
-// receiver of each entry of block b's concatenated runs; the runs are loaded into registers (16 B
-// per lane, up to RB runs per wave in flight together), and a per-receiver LDS counter hands out
-// slots in dst[slot][receiver].  The slot an entry lands in may differ between launches; every
-// receiver's multiset, and so the rule's result, does not.  Run padding is excluded through the
-// pad count kept in the low bits of each run's (16-byte aligned) stage start.
-template <int D, int T, bool WMSR = false, typename VT = double>
-__global__ __launch_bounds__(kBinSB) void k_bin_gather_of(const RoundArgs a, const VT* __restrict__ stage,
-                                                          const uint8_t* __restrict__ rid, uint32_t rstride,
-                                                          const uint2* __restrict__ tiles, uint32_t nrun, uint32_t Q,
-                                                          uint32_t Qc) {
-    constexpr uint32_t EPU = 16 / sizeof(VT);
-    constexpr uint32_t RB = 16;
-    constexpr uint32_t NW = kBinSB / 64;
-    constexpr uint32_t kRidCap = D * kBinSB + D * kBinSB / 16 * (EPU - 1);
-    __shared__ __attribute__((aligned(16))) VT dst[D * kBinSB + 64];         // + one dummy slot per lane
-    __shared__ __attribute__((aligned(16))) uint8_t lrid[kRidCap + 16];
-    __shared__ uint32_t cnt[kBinSB + 64];                                      // + one dummy counter per lane
-    InstState* S = a.st;
-    if (S->done) return;
-    const uint32_t b = a.qlo + (blockIdx.x & 7u) * Qc + (blockIdx.x >> 3);   // XCD-aware, as k_bin_gather
-    if (b >= a.qhi) return;
-    if (b >= Q) {
-        if (b < a.nblk && threadIdx.x == 0) a.partial[b] = make_double2(kInf, -kInf);
-        return;
-    }
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t li = (uint64_t)b * kBinSB + threadIdx.x;
-    const uint64_t i = a.row0 + li;
-    const bool live = li < a.nrows;
-    const VT xi = live ? reinterpret_cast<const VT*>(a.xin)[i] : VT(0);
-    cnt[threadIdx.x] = 0;
-    if (threadIdx.x < 64) cnt[kBinSB + threadIdx.x] = 0;
-    {   // block b's rid image -> LDS (rstride is a multiple of 16 and fits lrid)
-        const uint32_t n16 = rstride / 16;
-        const uint4* src = reinterpret_cast<const uint4*>(rid + (uint64_t)b * rstride) + threadIdx.x;
-        uint4* ld = reinterpret_cast<uint4*>(lrid) + (threadIdx.x & ~63u);
-        for (uint32_t o = 0; o < n16; o += kBinSB)
-            if (o + threadIdx.x < n16) __builtin_amdgcn_global_load_lds(src + o, ld + o, 16, 0, 0);
-    }
-    const uint2* tb = tiles + (uint64_t)b * (nrun + 1);
-    const uint4* s16 = reinterpret_cast<const uint4*>(stage);
-    const uint32_t r0 = w * nrun / NW, r1 = (w + 1) * nrun / NW;
-    const uint32_t nb = ((nrun + NW - 1) / NW + RB - 1) / RB;   // the same batch count in every wave
-    for (uint32_t it = 0; it < nb; ++it) {
-        const uint32_t g = r0 + it * RB;
-        const uint32_t ng = g < r1 ? (r1 - g < RB ? r1 - g : RB) : 0u;
-        uint32_t so_l = 0, pre_l = 0, nxt_l = 0;
-        if (lane < ng) {
-            const uint2 dd = tb[g + lane];
-            so_l = dd.x;
-            pre_l = dd.y;
-            nxt_l = tb[g + lane + 1].y;
-        }
-        // Loads with no control flow around them (a branch here makes the wait-count pass wait for
-        // every load in flight at the join): lanes past a run's end, and runs past ng (zero
-        // descriptors), re-read a valid address instead.
-        uint4 v0[RB], v1[RB];
-#pragma unroll
-        for (uint32_t k = 0; k < RB; ++k) {
-            const uint32_t so = __builtin_amdgcn_readlane(so_l, k), pre = __builtin_amdgcn_readlane(pre_l, k);
-            const uint32_t n16 = (__builtin_amdgcn_readlane(nxt_l, k) - pre) / EPU;
-            const uint4* sp = n16 ? s16 + so / EPU : s16;
-            v0[k] = sp[lane < n16 ? lane : 0u];
-            v1[k] = sp[64 + lane < n16 ? 64 + lane : 0u];
-        }
-        if (it == 0) __syncthreads();   // rid image and counters in place
-        // Consume in groups of 4 runs, each step issued for the whole group before the next (no
-        // branch in between): receiver ids from LDS, the slot atomics, the value writes.  Entries
-        // past a run's end (padding, idle lanes) go to a per-lane dummy counter and dummy slot.
-        using RT = typename std::conditional<EPU == 2, uint16_t, uint32_t>::type;   // EPU ids per read
-#pragma unroll
-        for (uint32_t k0 = 0; k0 < RB; k0 += 4) {
-            uint32_t rr[4][2][EPU];
-            VT vv[4][2][EPU];
-#pragma unroll
-            for (uint32_t k = k0; k < k0 + 4; ++k) {
-                const uint32_t so = __builtin_amdgcn_readlane(so_l, k), pre = __builtin_amdgcn_readlane(pre_l, k);
-                const uint32_t len = __builtin_amdgcn_readlane(nxt_l, k) - pre;
-                const uint32_t nreal = len - (so & (EPU - 1));   // 0 past ng
-#pragma unroll
-                for (uint32_t u = 0; u < 2; ++u) {
-                    const uint32_t e = (u * 64 + lane) * EPU;
-                    uint32_t pos = pre + e;
-                    pos = pos < kRidCap ? pos : 0u;
-                    const uint32_t ids = *reinterpret_cast<const RT*>(lrid + pos);
-                    __builtin_memcpy(vv[k - k0][u], u ? &v1[k] : &v0[k], 16);
-#pragma unroll
-                    for (uint32_t q = 0; q < EPU; ++q)
-                        rr[k - k0][u][q] = e + q < nreal ? (ids >> (8 * q)) & 0xFFu : kBinSB + lane;
-                }
-            }
-            uint32_t sl[4][2][EPU];
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k)
-#pragma unroll
-                for (uint32_t u = 0; u < 2; ++u)
-#pragma unroll
-                    for (uint32_t q = 0; q < EPU; ++q)
-                        sl[k][u][q] = __hip_atomic_fetch_add(&cnt[rr[k][u][q]], 1u, __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k)
-#pragma unroll
-                for (uint32_t u = 0; u < 2; ++u)
-#pragma unroll
-                    for (uint32_t q = 0; q < EPU; ++q) {
-                        const uint32_t r = rr[k][u][q];
-                        const uint32_t s2 = sl[k][u][q] < (uint32_t)D ? sl[k][u][q] : (uint32_t)D - 1;
-                        dst[r < kBinSB ? s2 * kBinSB + r : D * kBinSB + lane] = vv[k][u][q];
-                    }
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < RB; ++k) {   // runs longer than 128 units (rare)
-            if (k < ng) {
-                const uint32_t so = __builtin_amdgcn_readlane(so_l, k), pre = __builtin_amdgcn_readlane(pre_l, k);
-                const uint32_t len = __builtin_amdgcn_readlane(nxt_l, k) - pre;
-                const uint32_t n16 = len / EPU, nreal = len - (so & (EPU - 1));
-                const uint4* sp = s16 + so / EPU;
-                for (uint32_t o = 128; o < n16; o += 64) {
-                    if (o + lane < n16) {
-                        const uint4 u4 = sp[o + lane];
-                        VT val[EPU];
-                        __builtin_memcpy(val, &u4, 16);
-#pragma unroll
-                        for (uint32_t q = 0; q < EPU; ++q) {
-                            const uint32_t e = (o + lane) * EPU + q;
-                            if (e < nreal) {
-                                const uint32_t r = lrid[pre + e];
-                                const uint32_t s2 = atomicAdd(&cnt[r], 1u);
-                                dst[(s2 < (uint32_t)D ? s2 : (uint32_t)D - 1) * kBinSB + r] = val[q];
-                            }
-                        }
-                    }
-                }
-            }
-        }
-    }
-    __syncthreads();
-
-    double mn = kInf, mx = -kInf;
-    if (live) {
-        VT v[D + 1];
-        v[0] = xi;
-#pragma unroll
-        for (int t = 0; t < D; ++t) v[1 + t] = dst[t * kBinSB + threadIdx.x];
-        const VT res = apply_rule_reg<D, T, WMSR>(a.rule, v);
-        reinterpret_cast<VT*>(a.xout)[i] = res;
-        mn = res;
-        mx = res;
-    }
-    block_minmax_store<kBinSB>(mn, mx, a.partial + b, a.eacc);
 }
 
 // ------------------------------------------------------------------------------ plan build
@@ -1012,7 +847,7 @@ __device__ __forceinline__ uint64_t bin_run_key(const BinGeom& G, uint32_t b, ui
 
 // tiles[b][j] = (padded start | pad count, element offset inside block b's concatenated runs);
 // tiles[b][nrun] = (0, total).  Starts are multiples of the pad unit, so the low bits carry the
-// number of padding entries at the run's end (read by the order-free phase B).
+// number of padding entries at the run's end.
 __global__ __launch_bounds__(256) void k_bin_prefix(const uint32_t* __restrict__ pstart, const uint32_t* __restrict__ plen,
                                                     const uint2* __restrict__ tl, BinGeom G, uint32_t nrun,
                                                     uint2* __restrict__ tiles) {
@@ -1042,22 +877,6 @@ __global__ __launch_bounds__(256) void k_bin_inv(uint64_t E, BinGeom G, uint32_t
     const uint32_t j = G.levels == 1 ? key / G.Q : (key / G.QR) % G.K;
     const uint32_t pos = tiles[(uint64_t)b * (nrun + 1) + j].y + (uint32_t)(p - tl[key].x);
     invpos[(((uint64_t)b * (G.D / 8) + t / 8) * G.SB + (li % G.SB)) * 8 + (t & 7)] = (uint16_t)pos;
-}
-
-// rid[b][pos] = receiver (inside block b) of the entry at image position pos (order-free plans)
-__global__ __launch_bounds__(256) void k_bin_rid(uint64_t E, BinGeom G, uint32_t nrun, uint32_t rstride,
-                                                 const uint32_t* __restrict__ ks, const uint32_t* __restrict__ vs,
-                                                 const uint2* __restrict__ tl, const uint2* __restrict__ tiles,
-                                                 uint8_t* __restrict__ rid) {
-    const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (p >= E) return;
-    const uint32_t e = vs[p], key = ks[p];
-    if (key >= (G.levels == 1 ? G.none1 : G.none2)) return;
-    const uint64_t li = e / G.D;
-    const uint32_t b = (uint32_t)(li / G.SB);
-    const uint32_t j = G.levels == 1 ? key / G.Q : (key / G.QR) % G.K;
-    const uint32_t pos = tiles[(uint64_t)b * (nrun + 1) + j].y + (uint32_t)(p - tl[key].x);
-    rid[(uint64_t)b * rstride + pos] = (uint8_t)(li % G.SB);
 }
 
 // fix-up list: every sorted position p of the last level whose sender is not honest
@@ -1136,7 +955,6 @@ void binned_free(BinnedPlan& p) {
     (void)hipFree(p.pkA);
     (void)hipFree(p.idxM);
     (void)hipFree(p.invpos);
-    (void)hipFree(p.rid);
     (void)hipFree(p.tiles);
     (void)hipFree(p.mt);
     (void)hipFree(p.aoff);
@@ -1215,11 +1033,11 @@ hipError_t tile_sort(const uint32_t* ell, uint64_t E, const BinGeom& G, int leve
 }  // namespace
 
 hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t NR, uint32_t d, uint32_t dp,
-                        uint32_t sa, uint32_t sb, bool tagged, bool f32, bool ofree, hipStream_t s, bool var,
+                        uint32_t sa, uint32_t sb, bool tagged, bool f32, hipStream_t s, bool var,
                         const uint32_t* status, bool clean) {
-    if (var && (f32 || ofree)) return hipErrorNotSupported;   // CSR plans: fp64, invpos phase B
-    // receiver blocks other than kBinSB: clean invpos plans of a compiled (d, sb) pair only
-    if (sb != kBinSB && (var || ofree || tagged || !clean)) return hipErrorInvalidValue;
+    if (var && f32) return hipErrorNotSupported;   // CSR plans: fp64
+    // receiver blocks other than kBinSB: clean plans of a compiled (d, sb) pair only
+    if (sb != kBinSB && (var || tagged || !clean)) return hipErrorInvalidValue;
     hipError_t e = hipSuccess;
     uint32_t sr = 0;
     const uint32_t levels = binned_levels(N, NR, d, sa, sb, &sr);
@@ -1352,33 +1170,21 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
                            p.nrun, p.tiles);
         e = hipGetLastError();
     }
-    p.ofree = ofree;
     {
         const char* v = getenv("ACSIM_BIN_POL");
         p.pol = v ? (uint32_t)strtoul(v, nullptr, 0) & kPolMask
                   : kPolDefault | (G.levels == 2 ? kPolTwoLevelStores : kPolOneLevelStores);
     }
-    if (ofree) {   // order-free phase B: receiver ids in image order
-        p.rstride = ((uint32_t)d * sb + p.nrun * (G.pad - 1) + 15u) & ~15u;
-        if (e == hipSuccess) e = hipMalloc(&p.rid, (uint64_t)G.Q * p.rstride);
-        if (e == hipSuccess) e = hipMemsetAsync(p.rid, 0, (uint64_t)G.Q * p.rstride, s);
-        if (e == hipSuccess) {
-            hipLaunchKernelGGL(k_bin_rid, dim3(grid), dim3(256), 0, s, E, G, p.nrun, p.rstride, last->ks, last->vs,
-                               last->tl, p.tiles, p.rid);
-            e = hipGetLastError();
-        }
-    } else {
-        if (e == hipSuccess) e = hipMalloc(&p.invpos, Qp * d * 2);
-        if (e == hipSuccess) e = hipMemsetAsync(p.invpos, 0, Qp * d * 2, s);
-        if (e == hipSuccess) {
-            hipLaunchKernelGGL(k_bin_inv, dim3(grid), dim3(256), 0, s, E, G, p.nrun, last->ks, last->vs, last->tl,
-                               p.tiles, p.invpos);
-            e = hipGetLastError();
-        }
+    if (e == hipSuccess) e = hipMalloc(&p.invpos, Qp * d * 2);
+    if (e == hipSuccess) e = hipMemsetAsync(p.invpos, 0, Qp * d * 2, s);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_bin_inv, dim3(grid), dim3(256), 0, s, E, G, p.nrun, last->ks, last->vs, last->tl,
+                           p.tiles, p.invpos);
+        e = hipGetLastError();
     }
     // fault fix-up list: when the faulty senders' deliveries are few (at most an
     // eighth of all), their resolutions are written into the stage instead of tagging every sender
-    if (e == hipSuccess && tagged && status && !ofree && !getenv("ACSIM_BIN_NOFIX")) {
+    if (e == hipSuccess && tagged && status && !getenv("ACSIM_BIN_NOFIX")) {
         // two passes: count (cap 0), then fill a list of exactly that size
         uint32_t* cnt = nullptr;
         uint32_t n = 0;
@@ -1412,7 +1218,7 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     // allow 4 and a second pass only costs: 39.3 -> 43.8 us), and only when every part of every
     // block's image fits.  ACSIM_BIN_SPLIT=1..4 overrides (1: one pass).
     p.split = 1;
-    if (e == hipSuccess && !ofree) {
+    if (e == hipSuccess) {
         const char* v = getenv("ACSIM_BIN_SPLIT");
         uint32_t np = v ? (uint32_t)strtoul(v, nullptr, 10) : (!f32 && G.D == 32 ? 2u : 1u);
         if (np < 1 || np > 4 || var) np = 1;   // CSR plans: single pass (the VAR kernels)
@@ -1578,7 +1384,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
     // phase B writes a.partial[b] for each of its receiver blocks b < p.Q (and neutral pairs up to
     // a.nblk): partials sized for fewer blocks would be written past their slice
     if ((phases & 4u) && a.nblk < p.Q) return hipErrorInvalidValue;
-    if (p.SB != kBinSB && (!clean || p.var || p.ofree)) return hipErrorInvalidValue;
+    if (p.SB != kBinSB && (!clean || p.var)) return hipErrorInvalidValue;
     const uint32_t nslot_all = a.nblk > p.Q ? a.nblk : p.Q;
     if (a.qhi > nslot_all) a.qhi = nslot_all;
     if (a.qlo >= a.qhi) phases &= ~4u;
@@ -1616,13 +1422,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
 #define X(DD, TT)                                                                                        \
     if (p.D == DD && a.trim == TT) {                                                                     \
         if (p.SB != kBinSB) return launch_gather_sb<DD, TT, float>(p, a, st1, grid, Qc, pol, s);          \
-        if (p.ofree && a.rule == 4)                                                                      \
-            hipLaunchKernelGGL((k_bin_gather_of<DD, TT, true, float>), grid, dim3(kBinSB), 0, s, a, st1,    \
-                               p.rid, p.rstride, p.tiles, p.nrun, p.Q, Qc);                              \
-        else if (p.ofree)                                                                                \
-            hipLaunchKernelGGL((k_bin_gather_of<DD, TT, false, float>), grid, dim3(kBinSB), 0, s, a, st1,   \
-                               p.rid, p.rstride, p.tiles, p.nrun, p.Q, Qc);                              \
-        else if (fixp && a.rule == 4)                                                                    \
+        if (fixp && a.rule == 4)                                                                         \
             hipLaunchKernelGGL((k_bin_gather<DD, TT, true, false, float, 1, false, true>), grid, dim3(kBinSB), 0, \
                                s, a, st1, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                           \
         else if (fixp)                                                                                   \
@@ -1713,12 +1513,6 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
         else if (p.var)                                                                                  \
             hipLaunchKernelGGL((k_bin_gather<DD, TT, false, true, double, 1, true>), grid, dim3(kBinSB), 0, s, \
                                a, last, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol);                             \
-        else if (clean && p.ofree && w_)                                                                      \
-            hipLaunchKernelGGL((k_bin_gather_of<DD, TT, true>), grid, dim3(kBinSB), 0, s, a, last, p.rid,   \
-                               p.rstride, p.tiles, p.nrun, p.Q, Qc);                                     \
-        else if (clean && p.ofree)                                                                       \
-            hipLaunchKernelGGL((k_bin_gather_of<DD, TT>), grid, dim3(kBinSB), 0, s, a, last, p.rid,         \
-                               p.rstride, p.tiles, p.nrun, p.Q, Qc);                                     \
         else if (clean && p.split > 1 && w_)                                                             \
             ACS_BIN_NP_LAUNCH(DD, TT, true, double, last)                                                \
         else if (clean && p.split > 1)                                                                   \
