@@ -26,7 +26,11 @@ cpu_baseline times the CPU oracle (this repo's spec restatement, oracle/) on ran
 sample of the same workload.
 
 Extra legs (every N, each guarded: a failing leg is reported as an error string and never costs
-the headline line; a watchdog prints the line if a leg hangs):
+the headline line; each result, and at N > 1 each cfg5 sub-leg, enters the line as soon as it
+exists, and a watchdog prints the line — naming the stage that hung — if a leg hangs).  Exit code:
+0 when every leg ran and matched its golden hash, 4 when one failed or mismatched (`legs_failed`
+names them), 3 when the watchdog fired; the line is printed in every case and nothing is retried
+or re-launched:
   cfg4_f32          the headline workload in fp32 mode (north_star: "fp32 mode stated
                     separately"), timed and roofline-priced like the headline at 264 B/node-round,
                     100 FIXED rounds of a fresh handle checked against the oracle's hash.
@@ -236,6 +240,16 @@ class Ctx:
 
     def __init__(self, world, rank, local_rank, dev, group):
         self.world, self.rank, self.local_rank, self.dev, self.group = world, rank, local_rank, dev, group
+        self.stage = "headline"   # what is running (the watchdog's note names it)
+        self.partial = {}         # rank 0: the running leg's results so far (in the printed line)
+
+    def enter(self, stage: str) -> None:
+        """Mark the start of a (sub-)leg.  Fault injection for rehearsals (tools/):
+        ACSIM_BENCH_HANG=<stage> makes that stage hang on every rank, so the watchdog path can be
+        exercised on one box without a real hang."""
+        self.stage = stage
+        if os.environ.get("ACSIM_BENCH_HANG") == stage:
+            time.sleep(1e9)
 
     def barrier(self, sim=None):
         if sim is not None:
@@ -399,12 +413,13 @@ def _cfg5_handle(ctx: Ctx, cfg, xchunks):
             os.environ["ACSIM_XCHUNKS"] = old
 
 
-def _cfg5_sub(ctx: Ctx, warm: int, timed: int, xchunks) -> dict:
+def _cfg5_sub(ctx: Ctx, warm: int, timed: int, xchunks, stage: str = "cfg5_partitioned") -> dict:
     """Time one cfg5 exchange sequence on its own handle: `warm` + `timed` FIXED rounds, ms/round,
     the exchange share (the part of a round outside the rank's own round kernels) and sha256(x^10)
     against the golden hash."""
     import acsim
     from acsim.digest import sha256_values
+    ctx.enter(stage)
     cfg = acsim.preset("cfg5", max_rounds=warm + timed)
     sim = None
     err = None
@@ -456,20 +471,31 @@ def leg_cfg5(ctx: Ctx, warm: int = 2, timed: int = 8) -> dict:
                                f"timed rounds on one GPU (two-level binned exchange)")
             out["traffic"] = load_pmc_cfg5()
         return out
-    seqs = {}
+    # N > 1: the library's default sequence first (the all-gather), then the chunked one.  Each
+    # result lands in the printed line as soon as it exists (ctx.partial), so a later sub-leg that
+    # fails, mismatches the golden hash or hangs (the watchdog then prints the line and the process
+    # exits non-zero) never hides an earlier one; nothing is retried or re-launched.
+    seqs = ctx.partial.setdefault("sequences", {}) if ctx.rank == 0 else {}
     for name, xc in (("allgather", None), ("chunked", 4)):
         try:
-            seqs[name] = _cfg5_sub(ctx, warm, timed, xc)
+            res = _cfg5_sub(ctx, warm, timed, xc, stage=f"cfg5_partitioned.{name}")
         except Exception as e:  # noqa: BLE001
-            seqs[name] = {"error": f"{type(e).__name__}: {e}"}
+            res = {"error": f"{type(e).__name__}: {e}"}
+        if ctx.rank == 0:
+            seqs[name] = res
     if ctx.rank != 0:
         return {}
-    out = dict(seqs["allgather"])
+    # headline fields: the first sequence that ran and matched the golden hash (the default first)
+    ok = [n for n in ("allgather", "chunked") if seqs.get(n, {}).get("golden_match")]
+    out = dict(seqs[ok[0]]) if ok else {"error": "no cfg5 exchange sequence matched the golden hash"}
+    out["headline_sequence"] = ok[0] if ok else None
     out["workload"] = (f"cfg5: N=2^26 random 16-regular, trimmed t=5, FIXED; {warm} warm-up + {timed} timed "
-                       f"rounds, node-partitioned over {ctx.world} ranks; headline fields: the per-round RCCL "
-                       f"all-gather (default); `sequences` also times the chunked send / receive exchange")
+                       f"rounds, node-partitioned over {ctx.world} ranks; headline fields: the first golden-"
+                       f"matching sequence of the per-round RCCL all-gather (the library default) and the "
+                       f"chunked send / receive exchange; `sequences` holds both")
     out["traffic"] = None
     out["sequences"] = seqs
+    out["ok"] = len(ok) == 2
     return out
 
 
@@ -623,23 +649,34 @@ def main():
             printed[0] = True
 
     legs = [s for s in a.legs.split(",") if s]
+    failed = []
     if legs:
         def watchdog():
-            # the headline line is printed, but the run must not look clean: exit non-zero
-            emit(f"watchdog: legs unfinished after {a.leg_timeout:.0f} s")
+            # the headline line is printed (with every leg and sub-leg finished so far), but the run
+            # must not look clean: exit non-zero
+            emit(f"watchdog: {ctx.stage} unfinished after {a.leg_timeout:.0f} s")
             os._exit(3)
         timer = threading.Timer(a.leg_timeout, watchdog)
         timer.daemon = True
         timer.start()
         for name in legs:
             key, fn = LEGS[name]
+            ctx.enter(key)
+            ctx.partial = {"running": True}
+            if rank == 0:
+                out[key] = ctx.partial   # (replaced by the result; a hang prints what exists)
             try:
                 res = fn(ctx)
             except Exception as e:  # noqa: BLE001
                 res = {"error": f"{type(e).__name__}: {e}"}
             if rank == 0:
                 out[key] = res
+                if "error" in res or res.get("golden_match") is False or res.get("ok") is False:
+                    failed.append(key)
         timer.cancel()
+        ctx.stage = "cpu_baseline"
+    if rank == 0:
+        out["legs_failed"] = failed
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(n, a.cpu_seconds, a.dtype)
@@ -650,6 +687,8 @@ def main():
     if group is not None:
         group.barrier()
         group.close()
+    if failed:   # reported in the line above; the process must not look clean (no retry, no re-launch)
+        sys.exit(4)
 
 
 if __name__ == "__main__":
