@@ -654,6 +654,7 @@ def main():
         def watchdog():
             # the headline line is printed (with every leg and sub-leg finished so far), but the run
             # must not look clean: exit non-zero
+            out["legs_failed"] = failed + [ctx.stage]
             emit(f"watchdog: {ctx.stage} unfinished after {a.leg_timeout:.0f} s")
             os._exit(3)
         timer = threading.Timer(a.leg_timeout, watchdog)
