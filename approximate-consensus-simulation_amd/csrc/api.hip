@@ -617,6 +617,7 @@ static int enqueue_round(acs_sim* s, uint32_t r) {
             d.byz = s->c.byz_strategy;
             d.delta = s->mp.delta;
             d.bconst = s->mp.bconst;
+            d.f32 = s->f32 ? 1u : 0u;
             HIP_TRY(launch_round_dense(d, s->stream));
         } else if (s->c.topology != ACS_TOPO_CSR) {   // complete / regular graphs: one size for all
             if (s->generic_small) HIP_TRY(launch_round_generic(a, s->B, s->stream));
@@ -1036,8 +1037,9 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
 
     s->f32 = cfg->dtype == ACS_F32;
     s->es = s->f32 ? 4u : 8u;
-    // fp32 runs on the register, generic, batched (N <= 64), persistent dense
-    // (N <= 4096) and one-level binned kernels; the MFMA and two-kernel dense paths are fp64-only
+    // fp32 runs on the register, generic, batched (N <= 64), dense (persistent up to
+    // 4096 nodes, the two-kernel path up to 8192 since round 6) and binned kernels; the MFMA group
+    // kernel is fp64-only (its hardware-ordered sums would not keep fp32 rounds-to-convergence)
     if (cfg->topology == ACS_TOPO_COMPLETE && s->N <= kBatchedMaxN && cfg->delay_max == 0) {
         s->path = PATH_BATCHED;
         s->kname = batched_small_name((uint32_t)s->N, cfg->rule, cfg->fault_model != ACS_FAULT_NONE);
@@ -1049,8 +1051,7 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
                                          cfg->instance_offset);
         if (s->mfma) s->kname = "k_batched_mfma<v_mfma_f64_16x16x4>";
     } else if (cfg->topology == ACS_TOPO_COMPLETE && !partitioned && cfg->delay_max == 0 &&
-               (s->f32 ? s->N <= kDensePersistMaxN && !env_off("ACSIM_DENSE_PERSIST")   // fp32: persistent only
-                       : (s->B == 1 || (s->N <= kDensePersistMaxN && !env_off("ACSIM_DENSE_PERSIST")))) &&
+               (s->B == 1 || (s->N <= kDensePersistMaxN && !env_off("ACSIM_DENSE_PERSIST"))) &&
                dense_supported(cfg->fault_model, cfg->byz_strategy, cfg->rule, s->mp.thr, s->N)) {
         s->path = PATH_DENSE;
         s->dense_persist = s->N <= kDensePersistMaxN && !env_off("ACSIM_DENSE_PERSIST");

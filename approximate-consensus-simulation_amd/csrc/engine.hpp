@@ -276,6 +276,7 @@ struct DenseArgs {
     uint32_t* counts;         // [3] scratch: |B|, #Byzantine, #crash-silent
     uint32_t N, P, r, rule, trim, byz;
     double delta, bconst;
+    uint32_t f32;             // ACS_F32: x, xo and sorted hold binary32 values
 };
 bool dense_supported(uint32_t fault_model, uint32_t byz, uint32_t rule, uint32_t thr, uint64_t N);
 uint32_t dense_nblk(uint64_t N);

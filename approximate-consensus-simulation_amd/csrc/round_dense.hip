@@ -91,8 +91,12 @@ __device__ __forceinline__ void dense_bitonic(VT* sh, uint32_t P, VT (&v)[EMAX])
     }
 }
 
+// VT = double, or float in fp32 mode (binary32 values, the same sorted multiset)
+template <typename VT = double>
 __global__ __launch_bounds__(kDenseSortBlock) void k_dense_sort(const DenseArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double sh[];
+    extern __shared__ __attribute__((aligned(16))) unsigned char sh_raw[];
+    VT* sh = reinterpret_cast<VT*>(sh_raw);
+    const VT* x = reinterpret_cast<const VT*>(a.x);
     InstState* S = a.st;
     if (S->done) return;
     const uint32_t N = a.N, P = a.P, r = a.r;
@@ -101,11 +105,11 @@ __global__ __launch_bounds__(kDenseSortBlock) void k_dense_sort(const DenseArgs 
     __syncthreads();
     uint32_t nb = 0, nz = 0, ns = 0;
     for (uint32_t j = threadIdx.x; j < P; j += kDenseSortBlock) {
-        double v = kInf;
+        VT v = (VT)kInf;
         if (j < N) {
             const uint32_t st = a.status ? a.status[j] : kHonest;
             if (st == kHonest || (st != kByz && r < st)) {
-                v = a.x[j];
+                v = x[j];
                 ++nb;
             } else if (st == kByz) {
                 ++nz;
@@ -131,12 +135,13 @@ __global__ __launch_bounds__(kDenseSortBlock) void k_dense_sort(const DenseArgs 
     constexpr int EMAX = kGenericMaxM / kDenseSortBlock;   // 8
     const uint32_t E = (P + kDenseSortBlock - 1) / kDenseSortBlock;
     const uint32_t tid = threadIdx.x;
-    double v[EMAX];
+    VT v[EMAX];
     dense_bitonic<EMAX>(sh, P, v);
+    VT* sorted = reinterpret_cast<VT*>(a.sorted);
 #pragma unroll
     for (int e = 0; e < EMAX; ++e) {
         const uint32_t idx = tid + kDenseSortBlock * e;
-        if ((uint32_t)e < E && idx < cnt[0]) a.sorted[idx] = v[e];
+        if ((uint32_t)e < E && idx < cnt[0]) sorted[idx] = v[e];
     }
     if (threadIdx.x == 0) {
         a.counts[0] = cnt[0];
@@ -268,28 +273,40 @@ __device__ __forceinline__ VT dense_window(const Seq& M, uint32_t rule, uint32_t
     return res;
 }
 
+// receiver i's Byzantine value (SPLIT by parity, or CONSTANT): fp64 as §A.4, fp32 as spec.hpp
+// byz_value_f32 (Δ and c rounded to binary32 once, a binary32 add)
+__device__ __forceinline__ double dense_recv_byz(const DenseArgs& a, uint32_t i, double lo, double hi, double) {
+    return a.byz == 0 ? ((i & 1u) == 0 ? hi + a.delta : lo - a.delta) : a.bconst;
+}
+__device__ __forceinline__ float dense_recv_byz(const DenseArgs& a, uint32_t i, double lo, double hi, float) {
+    const float dl = (float)a.delta;
+    return a.byz == 0 ? ((i & 1u) == 0 ? (float)hi + dl : (float)lo - dl) : (float)a.bconst + 0.0f;
+}
+
+template <typename VT = double>
 __global__ __launch_bounds__(kDenseRecvBlock) void k_dense_recv(const DenseArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double shB[];   // the sorted base multiset
+    extern __shared__ __attribute__((aligned(16))) unsigned char shB_raw[];
+    VT* shB = reinterpret_cast<VT*>(shB_raw);   // the sorted base multiset
     InstState* S = a.st;
     if (S->done) return;
     {
         const uint32_t nb = a.counts[0];
-        for (uint32_t k = threadIdx.x; k < nb; k += kDenseRecvBlock) shB[k] = a.sorted[k];
+        const VT* sorted = reinterpret_cast<const VT*>(a.sorted);
+        for (uint32_t k = threadIdx.x; k < nb; k += kDenseRecvBlock) shB[k] = sorted[k];
         __syncthreads();
     }
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t i = blockIdx.x * (kDenseRecvBlock / 64) + (threadIdx.x >> 6);
     double mn = kInf, mx = -kInf;
     if (i < a.N) {
-        const double xi = a.x[i];
+        const VT xi = reinterpret_cast<const VT*>(a.x)[i];
         const uint32_t st = a.status ? a.status[i] : kHonest;
-        double res = xi;
+        VT res = xi;
         if (st == kHonest || (st != kByz && a.r < st)) {
             const uint32_t nb = a.counts[0], nz = a.counts[1], ns = a.counts[2];
-            const double lo = S->lo, hi = S->hi;
-            const double c = a.byz == 0 ? ((i & 1u) == 0 ? hi + a.delta : lo - a.delta) : a.bconst;
+            const VT c = dense_recv_byz(a, i, S->lo, S->hi, VT(0));
             // blocks (c, nz) and (xi, ns), ordered by value
-            Merged<> M;
+            Merged<VT> M;
             M.b = shB;
             const bool cfirst = c <= xi;
             M.v1 = cfirst ? c : xi;
@@ -305,7 +322,7 @@ __global__ __launch_bounds__(kDenseRecvBlock) void k_dense_recv(const DenseArgs 
                 mx = res;
             }
         }
-        if (lane == 0) a.xo[i] = res;
+        if (lane == 0) reinterpret_cast<VT*>(a.xo)[i] = res;
     }
     // lanes of a receiver agree; fold the block's receivers
     block_minmax_store<kDenseRecvBlock>(mn, mx, a.partial + blockIdx.x);
@@ -499,18 +516,26 @@ hipError_t launch_round_dense(const DenseArgs& a, hipStream_t s) {
     if (hipError_t e = hipGetDevice(&dev); e != hipSuccess) return e;
     if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
     std::call_once(once[dev], [dev] {
-        hipError_t e = hipFuncSetAttribute((const void*)k_dense_sort, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)(kGenericMaxM * sizeof(double)));
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)k_dense_recv, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)(kGenericMaxM * sizeof(double)));
+        hipError_t e = hipSuccess;
+        for (const void* f : {(const void*)k_dense_sort<double>, (const void*)k_dense_recv<double>,
+                              (const void*)k_dense_sort<float>, (const void*)k_dense_recv<float>})
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kGenericMaxM * sizeof(double)));
         status[dev] = e;
     });
     if (status[dev] != hipSuccess) return status[dev];
-    hipLaunchKernelGGL(k_dense_sort, dim3(1), dim3(kDenseSortBlock), a.P * sizeof(double), s, a);
+    if (a.N > kGenericMaxM || a.P > kGenericMaxM) return hipErrorNotSupported;   // (LDS images of P values)
+    const size_t es = a.f32 ? sizeof(float) : sizeof(double);
+    if (a.f32)
+        hipLaunchKernelGGL(k_dense_sort<float>, dim3(1), dim3(kDenseSortBlock), a.P * es, s, a);
+    else
+        hipLaunchKernelGGL(k_dense_sort<double>, dim3(1), dim3(kDenseSortBlock), a.P * es, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_dense_recv, dim3(dense_nblk(a.N)), dim3(kDenseRecvBlock), a.N * sizeof(double), s, a);
+    if (a.f32)
+        hipLaunchKernelGGL(k_dense_recv<float>, dim3(dense_nblk(a.N)), dim3(kDenseRecvBlock), a.N * es, s, a);
+    else
+        hipLaunchKernelGGL(k_dense_recv<double>, dim3(dense_nblk(a.N)), dim3(kDenseRecvBlock), a.N * es, s, a);
     return hipGetLastError();
 }
 

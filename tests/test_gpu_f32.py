@@ -89,6 +89,42 @@ def test_f32_complete_graphs_take_the_dense_kernel():
             assert g.kernel_name() == "k_dense_persist [f32]", (name, g.kernel_name())
 
 
+# fp32 on the two-kernel dense path (k_dense_sort + k_dense_recv, complete graphs above the
+# persistent kernel's 4096 nodes, up to 8192; round 6): Byzantine SPLIT with Δ, CONSTANT DLPSW and a
+# clean midpoint, a few FIXED rounds each (the oracle sorts 6-8 K entries per receiver per round)
+F32_DENSE_BIG = {
+    "dense6000_split_trim": Config(n_nodes=6000, topology="complete", rule="trimmed", trim=2000,
+                                   fault_model="byzantine", n_faulty=2000, byz_strategy="split", byz_delta=0.01,
+                                   termination="fixed", max_rounds=5, seed=51, trace_spread=True, dtype="f32"),
+    "dense4500_const_dlpsw": Config(n_nodes=4500, topology="complete", rule="dlpsw", trim=600,
+                                    fault_model="byzantine", n_faulty=600, byz_strategy="constant", byz_const=0.25,
+                                    termination="fixed", max_rounds=4, seed=52, trace_spread=True, dtype="f32"),
+    "dense8192_clean_mid": Config(n_nodes=8192, topology="complete", rule="midpoint", trim=1000,
+                                  termination="fixed", max_rounds=3, seed=53, trace_spread=True, dtype="f32"),
+}
+
+
+@pytest.mark.parametrize("name", list(F32_DENSE_BIG))
+def test_f32_dense_two_kernel_above_4096_matches_oracle(oracle_mod, name):
+    cfg = F32_DENSE_BIG[name]
+    with acsim.Simulator(cfg, device=0) as g:
+        assert g.kernel_name() == "k_dense_sort+k_dense_recv [f32]", g.kernel_name()
+    g, o = run_both(oracle_mod, cfg)
+    assert g["x"].dtype == np.float32
+    assert_same(g, o)
+
+
+@pytest.mark.parametrize("name", ["complete_trimmed_split", "dense_split_mid_delta"])
+def test_f32_dense_two_kernel_small_matches_oracle(oracle_mod, name, monkeypatch):
+    """The fp32 two-kernel dense path on the configs the persistent kernel serves, run to ε."""
+    monkeypatch.setenv("ACSIM_DENSE_PERSIST", "0")
+    cfg = CASES[name]
+    with acsim.Simulator(cfg, device=0) as g:
+        assert g.kernel_name() == "k_dense_sort+k_dense_recv [f32]", g.kernel_name()
+    g, o = run_both(oracle_mod, cfg)
+    assert_same(g, o)
+
+
 def test_f32_resume_and_chunks(oracle_mod):
     cfg = preset("cfg4_eps", n_nodes=4096, loss_p=0.1, dtype="f32", eps=1e-6)
     with acsim.Simulator(cfg, device=0) as g, oracle_mod.OracleSimulator(cfg, threads=8) as o:
