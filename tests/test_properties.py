@@ -293,6 +293,62 @@ def test_gpu_binned_exchange_random_configs(oracle_mod, case):
 
 
 @st.composite
+def block_size_cases(draw):
+    """Clean binned plans on a phase-B receiver block other than 256 (round 6):
+    t = 5, d = 16 / 32, the sort-based rules that take it, fp64 / fp32, one or two passes, one-
+    and two-level plans, and sometimes 2-4 virtual partitions with or without the chunked
+    exchange.  -> (cfg, source block size, receiver block, passes, partitions, chunks)"""
+    d = draw(st.sampled_from([16, 32]))
+    sb = draw(st.sampled_from([128, 512] if d == 16 else [128]))
+    cfg = Config(n_nodes=draw(st.integers(3000, 120000)), topology="random_regular", degree=d,
+                 rule=draw(st.sampled_from(["trimmed", "midpoint", "dlpsw"])), trim=5,
+                 eps=draw(st.sampled_from([1e-7, 1e-10])), max_rounds=draw(st.integers(1, 40)),
+                 termination=draw(st.sampled_from(["eps", "fixed"])),
+                 dtype=draw(st.sampled_from(["f64", "f64", "f32"])), seed=draw(st.integers(0, 2 ** 40)),
+                 trace_spread=True)
+    parts = draw(st.sampled_from([1, 1, 2, 3, 4]))
+    return (cfg, draw(st.sampled_from([512, 1024, 4096])), sb, draw(st.sampled_from(["", "1", "2"])), parts,
+            draw(st.sampled_from(["0", "2", "4"])))
+
+
+@pytest.mark.gpu
+@settings(max_examples=60, deadline=None, derandomize=True, database=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+@given(case=block_size_cases())
+def test_gpu_binned_block_size_random_configs(oracle_mod, case):
+    """The binned exchange on 128 / 512-receiver phase-B blocks, whole and node-partitioned,
+    against the oracle bit for bit (every private copy of x under partitions)."""
+    import os
+    import acsim
+    cfg, sa, sb, split, parts, xchunks = case
+    env = {"ACSIM_BIN_SA": str(sa), "ACSIM_BIN_SB": str(sb), "ACSIM_BIN_SPLIT": split, "ACSIM_XCHUNKS": xchunks}
+    old = {k: os.environ.get(k) for k in env}
+    for k, v in env.items():
+        if v:
+            os.environ[k] = v
+        else:
+            os.environ.pop(k, None)
+    try:
+        with acsim.Simulator(cfg, device=0, partitions=parts) as g:
+            name = g.kernel_name()
+            g.run()
+            gr, gt = g.rounds(), g.spread_trace(0)
+            copies = [g.partition_values(q) for q in range(parts)] if parts > 1 else [g.values(0)]
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert "k_bin_" in name and f" sb{sb}" in name, (cfg, sa, sb, name)
+    o = _run_oracle(oracle_mod, cfg.replace(omp_threads=16))
+    assert np.array_equal(gr, o["rounds"]), (cfg, sa, sb, split, parts, name)
+    assert np.array_equal(_bits(gt), _bits(o["trace"][0])), (cfg, sa, sb, split, parts, name)
+    for q, x in enumerate(copies):
+        assert np.array_equal(_bits(x), _bits(o["x"][0])), (cfg, sa, sb, split, parts, q, name)
+
+
+@st.composite
 def partition_cases(draw):
     """Node-partitioned runs (SURVEY §8(e), cfg5's data flow) on virtual partitions: a binned or
     per-lane config, 2-8 row blocks, the chunked or the all-gather exchange, small source blocks."""
