@@ -717,27 +717,29 @@ static constexpr unsigned kPolledHostFlags = hipHostMallocMapped | hipHostMalloc
 // Poll a host-mapped sequence number a launch on s->stream releases at system scope.  The stream is
 // queried every 256 spins, so a failed launch returns its error rather than spinning forever.
 // patient: the wait may span a whole chunk of long rounds (EPS chunk verdicts of large graphs,
-// milliseconds each): after 100 us of spinning the host sleeps 20 us between polls instead of
-// holding a core (ranks share the box's cores; the extra wake-up latency is well under 1 % of such a
-// chunk).  The short call-end reads spin throughout (their wait is a few microseconds).
+// milliseconds each): after 100 us of spinning the host yields the core between polls
+// (sched_yield), so ranks and threads sharing the box's cores run meanwhile, without adding the
+// wake-up latency of a sleep (a 20 us sleep_for, with the kernel's default timer slack, added
+// ≈ 60 us to every cfg4 EPS run: profiles/r06_eps_yield_configs.jsonl).  The short call-end reads
+// spin throughout (their wait is a few microseconds).
 static int wait_mapped_seq(acs_sim* s, const unsigned long long* p, unsigned long long seq, const char* what,
                            bool patient = false) {
     const auto t0 = std::chrono::steady_clock::now();
-    bool sleeping = false;
+    bool yielding = false;
     for (uint32_t it = 1;; ++it) {
         if (__atomic_load_n(p, __ATOMIC_ACQUIRE) == seq) return ACS_OK;
-        if (sleeping || (it & 255u) == 0) {
+        if ((it & 255u) == 0) {
             const hipError_t q = hipStreamQuery(s->stream);
             if (q == hipSuccess) {
                 if (__atomic_load_n(p, __ATOMIC_ACQUIRE) == seq) return ACS_OK;
                 return fail(ACS_EDEVICE, "%s: stream idle without the sequence number", what);
             }
             if (q != hipErrorNotReady) return fail(ACS_EDEVICE, "%s: %s", what, hipGetErrorString(q));
-            if (patient && !sleeping && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(100))
-                sleeping = true;
+            if (patient && !yielding && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(100))
+                yielding = true;
         }
-        if (sleeping)
-            std::this_thread::sleep_for(std::chrono::microseconds(20));
+        if (yielding)
+            std::this_thread::yield();
         else
             __builtin_ia32_pause();
     }
