@@ -49,14 +49,16 @@ def test_both_sequences_match(monkeypatch):
     # the all-gather result was already in the printed line while the chunked sub-leg ran
     assert "allgather" in seen[1][2] and seen[1][2]["allgather"]["ms_per_round"] == 2.0
     assert out["headline_sequence"] == "allgather" and out["ms_per_round"] == 2.0
-    assert out["ok"] is True and set(out["sequences"]) == {"allgather", "chunked"}
+    assert out["ok"] is True and out["opt_in_ok"] is True and set(out["sequences"]) == {"allgather", "chunked"}
 
 
-def test_chunked_mismatch_keeps_allgather_and_fails_the_leg(monkeypatch):
+def test_chunked_mismatch_keeps_allgather_and_is_reported(monkeypatch):
+    """The opt-in chunked sequence failing is reported (opt_in_ok) but does not fail the leg: the
+    default sequence's result stands and the run keeps its exit code."""
     out, _, _ = run_leg(monkeypatch, {"allgather": {"golden_match": True, "ms_per_round": 2.0},
                                       "chunked": {"golden_match": False, "ms_per_round": 1.0}})
     assert out["headline_sequence"] == "allgather" and out["ms_per_round"] == 2.0
-    assert out["ok"] is False
+    assert out["ok"] is True and out["opt_in_ok"] is False
 
 
 def test_allgather_error_falls_back_to_chunked(monkeypatch):
@@ -64,7 +66,7 @@ def test_allgather_error_falls_back_to_chunked(monkeypatch):
                                       "chunked": {"golden_match": True, "ms_per_round": 1.0}})
     assert out["sequences"]["allgather"]["error"].startswith("RuntimeError: ECOMM")
     assert out["headline_sequence"] == "chunked" and out["ms_per_round"] == 1.0
-    assert out["ok"] is False
+    assert out["ok"] is False and out["opt_in_ok"] is True   # the default sequence failed: the leg fails
 
 
 def test_no_sequence_matches(monkeypatch):
