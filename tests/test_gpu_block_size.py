@@ -9,6 +9,7 @@ Every case below would fail on the old sizing (the guard returns an error, or th
 half the blocks).  Bar: bit-exact against the oracle or the oracle-written golden hashes.
 """
 import contextlib
+import json
 import os
 
 import numpy as np
@@ -21,8 +22,7 @@ from acsim.digest import sha256_values
 pytestmark = pytest.mark.gpu
 
 THREADS = max(1, min(16, os.cpu_count() or 1))
-GOLDEN = __import__("json").load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
-                                                   "fullsize.json")))
+GOLDEN = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fullsize.json")))
 
 
 @contextlib.contextmanager
