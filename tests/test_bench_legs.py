@@ -1,7 +1,7 @@
 """bench.py's multi-rank leg logic on the CPU (no GPU, no RCCL): the cfg5 leg at N > 1 reports
 each exchange sequence as it finishes, takes its headline fields from the first golden-matching
-sequence, and marks the leg failed when a sequence errs or mismatches (VERDICT r05
-item 5).  The sub-legs are stubbed; the real ones run on the GPU box (bench.py, rehearsal in
+sequence, and marks the leg failed when the default (all-gather) sequence errs or mismatches; the
+opt-in chunked sequence's result is reported as opt_in_ok.  The sub-legs are stubbed; the real ones run on the GPU box (bench.py, rehearsal in
 tools/sessions_scripts/r06_rehearsal.sh)."""
 import os
 import sys
