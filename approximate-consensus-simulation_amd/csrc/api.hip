@@ -585,8 +585,9 @@ static int enqueue_round(acs_sim* s, uint32_t r) {
     // workgroups would stop on a stale verdict while workgroup 0 streams.  Hub rows (generic
     // kernel partials) and partitioned rounds are therefore excluded here;
     // tests/test_gpu_binned.py::test_eps_publication_in_every_gather_variant covers each form.
+    // (narrow plans publish in every round: the next phase A chooses its stage width from the pair)
     unsigned long long* pub = s->eacc && s->binned && s->defer_fin && !s->n_hub && !s->partitioned &&
-                                      s->c.termination == ACS_TERM_EPS
+                                      (s->c.termination == ACS_TERM_EPS || s->bin.narrow)
                                   ? s->eacc + kEaccWords * ((r + 1) & 1u)
                                   : nullptr;
     if (!s->partitioned) {
@@ -1245,10 +1246,14 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
         // per receiver block): then every partition keeps its ELL and runs the per-lane kernel,
         // which serves the same configs (binned_supported implies a compiled register variant).
         bool bin_refused = false;
+        // narrow stage (ACSIM_BIN_NARROW=1, opt-in): whole unpartitioned rounds with
+        // the deferred finalize, whose phase B publishes each round's (min, max) for the next phase A
+        const char* nar_env = getenv("ACSIM_BIN_NARROW");
+        const bool want_narrow = nar_env && nar_env[0] == '1' && !partitioned && s->defer_fin && s->eacc;
         auto try_plan = [&](BinnedPlan& plan, const uint32_t* ell, uint64_t nr) -> hipError_t {
             if (!s->binned || bin_refused || !nr) return hipSuccess;
             hipError_t e = binned_build(plan, ell, s->N, nr, s->d, s->dp, bin_sa, bin_sb, tagged, s->f32, s->stream,
-                                        false, s->status, s->clean);
+                                        false, s->status, s->clean, want_narrow);
             if (e == hipErrorNotSupported) {
                 bin_refused = true;
                 return hipSuccess;
@@ -1282,6 +1287,8 @@ static int create_impl(const acs_config* cfg, int device, int nranks, int rank, 
                 s->kname += " split" + std::to_string(s->bin.split);
             if (s->bin.pkA)   // 14-bit packed phase-A index stream
                 s->kname += " pk14A";
+            if (s->bin.narrow)   // narrow stage
+                s->kname += " narrow";
             if (s->bin.fix) {   // fault fix-up list instead of tagged senders
                 const size_t pos = s->kname.find("+k_bin_tag");
                 if (pos != std::string::npos) s->kname.replace(pos, 10, "+k_bin_fixup");

@@ -210,10 +210,27 @@ __device__ __forceinline__ uint32_t pk14_at(const uint32_t* __restrict__ pk, uin
 // waves in turn (wave w takes blocks mb + w, mb + w + NW, ...), software-pipelined like
 // bin_stream_t (the next block's four index loads are issued before this block's gathers and
 // stores); the partial blocks at the ends go position by position.
-template <uint32_t SMODE, typename VT = double>
+// NAR (narrow stage, fp64 plans): out holds u32 entries, the low word of each
+// value's bits minus the low word of the round's base (nar_lo); only the low word is read from LDS.
+template <uint32_t SMODE, typename VT = double, bool NAR = false>
 __device__ __forceinline__ void bin_stream_pk14_t(const VT* lx, const uint32_t* __restrict__ pk,
-                                                  VT* __restrict__ out, uint64_t p0, uint64_t p1) {
-    using V2 = decltype(bin_pair(VT(0), VT(0)));
+                                                  std::conditional_t<NAR, uint32_t, VT>* __restrict__ out,
+                                                  uint64_t p0, uint64_t p1, uint32_t nar_lo = 0) {
+    static_assert(!NAR || sizeof(VT) == 8, "the narrow stage encodes fp64 values");
+    using V2 = std::conditional_t<NAR, uint2, decltype(bin_pair(VT(0), VT(0)))>;
+    const uint32_t* l32 = reinterpret_cast<const uint32_t*>(lx);   // (NAR: the low words)
+    auto one = [&](uint32_t k) {
+        if constexpr (NAR)
+            return l32[2 * k] - nar_lo;
+        else
+            return lx[k];
+    };
+    auto pair = [&](uint32_t k0, uint32_t k1) -> V2 {
+        if constexpr (NAR)
+            return make_uint2(one(k0), one(k1));
+        else
+            return bin_pair(lx[k0], lx[k1]);
+    };
     // V2 units per 1 GiB window: the descriptor's num_records (0x7FFFFFF0) must cover the whole window
     // plus one V2 (with 2 GiB windows the last pair of each window sat at offset 0x7FFFFFF0 and its
     // store failed the range check silently; stages above 2 GiB are two-level, cfg5-sized plans)
@@ -249,10 +266,9 @@ __device__ __forceinline__ void bin_stream_pk14_t(const VT* lx, const uint32_t* 
                 // bank-conflict-free LDS reads (consecutive 8-byte words across the wave)
                 const uint32_t x0 = pk14_extract(c0, c1, c2, ch, 2 * q), x1 = pk14_extract(c0, c1, c2, ch, 2 * q + 1);
                 asm volatile("" ::"v"(x0), "v"(x1));
-                const V2 v = bin_pair(lx[(q * 128u + lane) & 16383u], lx[(q * 128u + 64u + lane) & 16383u]);
+                const V2 v = pair((q * 128u + lane) & 16383u, (q * 128u + 64u + lane) & 16383u);
 #else
-                const V2 v = bin_pair(lx[pk14_extract(c0, c1, c2, ch, 2 * q)],
-                                      lx[pk14_extract(c0, c1, c2, ch, 2 * q + 1)]);
+                const V2 v = pair(pk14_extract(c0, c1, c2, ch, 2 * q), pk14_extract(c0, c1, c2, ch, 2 * q + 1));
 #endif
                 const uint64_t vi = m * 256 + q * 64 + lane;   // pair index of positions 2vi, 2vi + 1
                 if constexpr (SMODE == 2) {
@@ -273,9 +289,9 @@ __device__ __forceinline__ void bin_stream_pk14_t(const VT* lx, const uint32_t* 
     }
     // partial blocks at both ends (or the whole range when it holds no full block)
     const uint64_t h1 = mb < me ? (mb << 9) : p1;
-    for (uint64_t q = p0 + threadIdx.x; q < h1; q += blockDim.x) out[q] = lx[pk14_at(pk, q)];
+    for (uint64_t q = p0 + threadIdx.x; q < h1; q += blockDim.x) out[q] = one(pk14_at(pk, q));
     if (mb < me)
-        for (uint64_t q = (me << 9) + threadIdx.x; q < p1; q += blockDim.x) out[q] = lx[pk14_at(pk, q)];
+        for (uint64_t q = (me << 9) + threadIdx.x; q < p1; q += blockDim.x) out[q] = one(pk14_at(pk, q));
 }
 
 template <typename VT>
@@ -287,6 +303,37 @@ __device__ __forceinline__ void bin_stream_pk14(const VT* lx, const uint32_t* __
         bin_stream_pk14_t<2, VT>(lx, pk, out, p0, p1);
     else
         bin_stream_pk14_t<0, VT>(lx, pk, out, p0, p1);
+}
+
+// the narrow stage's stream (u32 entries; fp64 plans)
+__device__ __forceinline__ void bin_stream_pk14_narrow(const double* lx, const uint32_t* __restrict__ pk,
+                                                       uint32_t* __restrict__ out, uint64_t p0, uint64_t p1,
+                                                       uint32_t smode, uint32_t nar_lo) {
+    if (smode == 1)
+        bin_stream_pk14_t<1, double, true>(lx, pk, out, p0, p1, nar_lo);
+    else if (smode == 2)
+        bin_stream_pk14_t<2, double, true>(lx, pk, out, p0, p1, nar_lo);
+    else
+        bin_stream_pk14_t<0, double, true>(lx, pk, out, p0, p1, nar_lo);
+}
+
+// Narrow stage: the stage entry width of a round from the exact (min, max) of
+// x^r the previous phase B published (omin = ord(min), omax = ord(max); resolve.hpp ord_of).  When
+// every value lies strictly on one side of zero, bit patterns are monotone in value, so every x^r
+// is base + k with 0 <= k <= omax - omin (base: the smaller pattern, i.e. the min for positive
+// values and the max for negative ones); with that span below 2^32, a u32 offset carries each
+// value exactly.  w = 8: full width (nothing published, a zero or mixed signs, or a wider span).
+__device__ __forceinline__ void narrow_choose(unsigned long long omin, unsigned long long omax, uint32_t& w,
+                                              unsigned long long& base) {
+    constexpr unsigned long long kOrdPos0 = 1ull << 63;      // ord(+0.0)
+    constexpr unsigned long long kOrdNeg0 = ~(1ull << 63);   // ord(-0.0)
+    w = 8;
+    base = 0;
+    if (omin > omax) return;   // nothing published (the pair's identity decodes to NaNs)
+    const bool pos = omin > kOrdPos0, neg = omax < kOrdNeg0;
+    if (!(pos || neg) || omax - omin > 0xFFFFFFFFull) return;
+    w = 4;
+    base = pos ? (omin & ~kOrdPos0) : ~omax;
 }
 
 // Copy runs [r0, r1) of a run table (start in `src` elements, element offset `pre` in the LDS

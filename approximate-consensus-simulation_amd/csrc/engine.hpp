@@ -75,6 +75,9 @@ struct RoundArgs {
     // (min, max) into eacc[0] = max ~ord(min), eacc[1] = max ord(max) (ord: order-preserving bits,
     // identity 0), so the next phase A's workgroups can stop without the block partials
     unsigned long long* eacc;
+    // narrow stage (binned phase B of narrow plans): {base lo, base hi, entry
+    // width 4 or 8, 0}, written by this round's phase A (BinnedPlan::nhdr; launch_round_binned sets it)
+    const uint4* nhdr;
 };
 constexpr uint32_t kEaccSlots = 32, kEaccStride = 16;       // eacc pairs, u64 words between pairs
 constexpr uint32_t kEaccWords = kEaccSlots * kEaccStride;   // eacc words of one round parity
@@ -212,6 +215,11 @@ struct BinnedPlan {
     // delivery from a sender that is not honest; nullptr: tagged senders (k_bin_tag) instead
     uint4* fix = nullptr;
     uint32_t nfix = 0;
+    // narrow stage (ACSIM_BIN_NARROW=1; clean one-level fp64 plans): a round whose
+    // values all lie strictly on one side of zero within 2^32 ulps of each other stages u32 offsets
+    // from their base instead of 8-byte values; runs are then padded to 4 entries
+    bool narrow = false;
+    uint4* nhdr = nullptr;              // the round's {base, width} (phase A writes, phase B reads)
 };
 bool binned_supported(uint32_t d, uint32_t t, uint32_t rule);
 // 1 or 2 exchange levels for NR local receivers of an N-node graph (0: not supported); sb = receiver block.
@@ -219,9 +227,10 @@ uint32_t binned_levels(uint64_t N, uint64_t NR, uint32_t d, uint32_t sa, uint32_
 // Builds the plan from the ELL of the NR local rows (sorted or spec order; slot-dependent configs
 // need spec order); sa = source block size; sb = receiver block (binned_block_size; must satisfy
 // binned_sb_supported); tagged: the config has a fault schedule.
+// narrow: build a narrow plan where the plan qualifies (p.narrow says whether it did).
 hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t NR, uint32_t d, uint32_t dp,
                         uint32_t sa, uint32_t sb, bool tagged, bool f32, hipStream_t s, bool var = false,
-                        const uint32_t* status = nullptr, bool clean = false);
+                        const uint32_t* status = nullptr, bool clean = false, bool narrow = false);
 void binned_free(BinnedPlan& p);
 // clean: no slot-dependent decision (selects the plain phase-B instantiation)
 // fin: the previous round's finalize, deferred into this round's phase A (nullptr: none pending)

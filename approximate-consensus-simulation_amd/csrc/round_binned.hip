@@ -55,7 +55,7 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
                                                      uint32_t segs, uint32_t chunk, uint32_t pol,
                                                      const FinalizeArgs fin, uint32_t fin_on, const SrcSel sel,
                                                      uint64_t* __restrict__ ts, unsigned long long* __restrict__ ereset,
-                                                     const uint32_t* __restrict__ pkA) {
+                                                     const uint32_t* __restrict__ pkA, uint4* __restrict__ nhdr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lx_raw[];
     VT* lx = reinterpret_cast<VT*>(lx_raw);
     if (st->done) return;
@@ -98,7 +98,8 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
         }
     }
     const bool idle = noblk || p0 >= p1;
-    if (idle && !(fin_on && blockIdx.x == 0)) return;
+    // (workgroup 0 always records the deferred finalize and, on narrow plans, the round's width)
+    if (idle && !(blockIdx.x == 0 && (fin_on || nhdr))) return;
     const uint64_t base = (uint64_t)a * SA;
     const uint32_t n = idle ? 0u : (uint32_t)(N - base < SA ? N - base : SA);
     {   // x block -> LDS by LDS-DMA, 16 B per lane (x is allocated with spare elements, so the
@@ -109,6 +110,40 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
         uint4* ld = reinterpret_cast<uint4*>(lx) + (threadIdx.x & ~63u);
         for (uint32_t o = 0; o < n16; o += kBinA)
             if (o + threadIdx.x < n16) __builtin_amdgcn_global_load_lds(xs + o, ld + o, 16, 0, 0);
+    }
+    // The (min, max) of x^r the previous phase B published (fin.eacc; plain loads: its atomics
+    // completed before this launch began, and the kernel boundary makes them visible here as it
+    // does x^r itself): the EPS verdict of workgroups other than 0, and on narrow plans (nhdr) the
+    // round's stage entry width, which workgroup 0 records for phase B.  Every
+    // workgroup reads the same pair, so all of them choose the same width.
+    __shared__ uint32_t pub_done, nar_w;
+    __shared__ unsigned long long nar_base;
+    const bool pub_in = fin_on && fin.eacc;
+    if (fin_on || nhdr) {
+        if (threadIdx.x < 64) {
+            unsigned long long lo = 0, hi = 0;
+            if (pub_in && threadIdx.x < kEaccSlots) {
+                lo = fin.eacc[threadIdx.x * kEaccStride];
+                hi = fin.eacc[threadIdx.x * kEaccStride + 1];
+            }
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {
+                const unsigned long long l2 = __shfl_xor(lo, o, 64), h2 = __shfl_xor(hi, o, 64);
+                lo = l2 > lo ? l2 : lo;
+                hi = h2 > hi ? h2 : hi;
+            }
+            if (threadIdx.x == 0) {
+                const double mn = ord_inv(~lo), mx = ord_inv(hi);
+                const double spread = fin.f32 ? (double)(float)(mx - mn) : mx - mn;
+                pub_done = pub_in && fin.term_eps && spread <= fin.eps ? 1u : 0u;
+                uint32_t w = 8;
+                unsigned long long base = 0;
+                if (nhdr && pub_in) narrow_choose(~lo, hi, w, base);
+                nar_w = w;
+                nar_base = base;
+                if (nhdr && blockIdx.x == 0) *nhdr = make_uint4((uint32_t)base, (uint32_t)(base >> 32), w, 0u);
+            }
+        }
     }
     if (fin_on) {
         // deferred finalize of the previous round.  Only workgroup 0 folds the
@@ -124,27 +159,6 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
         if (blockIdx.x == 0) {
             done = fold_partials<false, kBinA>(fin, 0, true);
         } else {
-            // (plain loads: the previous phase B's atomics completed before this launch began, and
-            // the kernel boundary makes them visible here as it does x^r itself)
-            __shared__ uint32_t pub_done;
-            if (threadIdx.x < 64) {
-                unsigned long long lo = 0, hi = 0;
-                if (fin.eacc && threadIdx.x < kEaccSlots) {
-                    lo = fin.eacc[threadIdx.x * kEaccStride];
-                    hi = fin.eacc[threadIdx.x * kEaccStride + 1];
-                }
-#pragma unroll
-                for (int o = 32; o >= 1; o >>= 1) {
-                    const unsigned long long l2 = __shfl_xor(lo, o, 64), h2 = __shfl_xor(hi, o, 64);
-                    lo = l2 > lo ? l2 : lo;
-                    hi = h2 > hi ? h2 : hi;
-                }
-                if (threadIdx.x == 0) {
-                    const double mn = ord_inv(~lo), mx = ord_inv(hi);
-                    const double spread = fin.f32 ? (double)(float)(mx - mn) : mx - mn;
-                    pub_done = fin.eacc && fin.term_eps && spread <= fin.eps ? 1u : 0u;
-                }
-            }
             __syncthreads();
             done = pub_done != 0u || fin.r_next >= fin.max_rounds;
         }
@@ -155,6 +169,13 @@ __global__ __launch_bounds__(kBinA) void k_bin_scatter(const VT* __restrict__ x,
     const uint64_t t1 = ts ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint32_t smode = (pol & kPolSc1Store) ? 2u : (pol & kPolNtStore) ? 1u : 0u;
     if (pkA) {   // 14-bit packed indices
+        if constexpr (sizeof(VT) == 8) {
+            if (nhdr && nar_w == 4u) {   // narrow stage: u32 offsets from the round's base
+                bin_stream_pk14_narrow(lx, pkA, reinterpret_cast<uint32_t*>(stage), p0, p1, smode, (uint32_t)nar_base);
+                if (ts) bin_ts(ts, t0, t1);
+                return;
+            }
+        }
         bin_stream_pk14(lx, pkA, stage, p0, p1, smode);
         if (ts) bin_ts(ts, t0, t1);
         return;
@@ -271,14 +292,49 @@ __global__ __launch_bounds__(256) void k_bin_fixup(const uint4* __restrict__ fix
 // delivery (k_bin_fixup), a missing one as a quiet NaN; phase B draws the §A.5 drop mask, turns
 // dropped and NaN entries into missing ones and applies the receiver's own status — no tag
 // decoding, no Byzantine draws, clean-kernel registers.
+// x^{r+1}_i, plain or write-through (kPolSc1X: no dirty x lines left in L2 at the kernel boundary)
+template <int SB, typename VT>
+__device__ __forceinline__ void bin_store_x(const RoundArgs& a, uint64_t i, VT res, uint32_t pol) {
+    if (pol & kPolSc1X) {
+        const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<VT*>(a.xout) + (i - threadIdx.x), 0, (int)(SB * sizeof(VT)), 0x00020000);
+        if constexpr (sizeof(VT) == 8) {
+            using UV = unsigned int __attribute__((ext_vector_type(2)));
+            UV bits;
+            __builtin_memcpy(&bits, &res, 8);
+            __builtin_amdgcn_raw_buffer_store_b64(bits, rx, threadIdx.x * 8u, 0, 16);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, res), rx, threadIdx.x * 4u, 0, 16);
+        }
+    } else {
+        reinterpret_cast<VT*>(a.xout)[i] = res;
+    }
+}
+
+// The narrow header as a scalar load (constant address space: phase A wrote it before this launch
+// and nothing writes it during one, so the scalar cache may serve it; as a vector load the compiler
+// made every workgroup wait for it alone before its first copies)
+__device__ __forceinline__ uint4 bin_nhdr_load(const uint4* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const __attribute__((address_space(4))) uint32_t* q = (const __attribute__((address_space(4))) uint32_t*)p;
+    return make_uint4(q[0], q[1], q[2], q[3]);
+#else
+    return *p;
+#endif
+}
+
+// NAR (narrow plans; clean fp64 only): each round reads the stage entry width
+// phase A chose (a.nhdr); in a 4-byte round the whole image of u32 offsets is copied in one pass
+// into the same LDS and every pick-up adds the round's base to recover the value's bits.
 template <int D, int T, bool WMSR = false, bool FAULTY = false, typename VT = double, int NP = 1, bool VAR = false,
-          bool FIX = false, int SB = (int)kBinSB>
-__global__ __launch_bounds__(SB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) : FIX && NP > 1 && (T || WMSR) ? 4 : 1) void k_bin_gather(const RoundArgs a, const VT* __restrict__ stage,
+          bool FIX = false, int SB = (int)kBinSB, bool NAR = false>
+__global__ __launch_bounds__(SB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) : (FIX || NAR) && NP > 1 && (T || WMSR) ? 4 : 1) void k_bin_gather(const RoundArgs a, const VT* __restrict__ stage,
                                                        const uint16_t* __restrict__ invpos,
                                                        const uint2* __restrict__ tiles, uint32_t nrun, uint32_t Q,
                                                        uint32_t Qc, uint32_t pol) {
     static_assert(D % 8 == 0, "invpos is read 8 slots at a time");
     static_assert(!(FIX && FAULTY), "FIX replaces the tagged resolution");
+    static_assert(!NAR || (sizeof(VT) == 8 && !FAULTY && !FIX && !VAR), "narrow stages: clean fp64 plans");
     constexpr bool FLT = FAULTY || FIX;   // a fault schedule or loss: receiver status and drop mask
     // runs are padded to 16-byte multiples; nrun <= D*SB/16 (checked when the plan is built)
     __shared__ __attribute__((aligned(16)))
@@ -304,6 +360,11 @@ __global__ __launch_bounds__(SB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) :
         if (live && a.deg[i] == kDegHub) live = false;
     }
     const uint2* tb = tiles + (uint64_t)b * (nrun + 1);
+    // narrow plans: this round's stage entry width (4: u32 offsets from the base in .x/.y), read
+    // after the first loads this workgroup needs anyway, so that one wait covers both (read first,
+    // it was waited for alone ahead of them: phase B +4-5 us in 8-byte rounds)
+    uint4 nh = make_uint4(0u, 0u, 8u, 0u);
+    bool nar = false;
     // NP-pass blocks of at most 64 runs: every wave fetches all descriptors first (one per lane)
     // and issues part 0's DMA before anything else is in flight, so the only wait ahead of the
     // first transfer is the descriptor load itself; later parts issue from registers.
@@ -326,17 +387,23 @@ __global__ __launch_bounds__(SB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) :
             pdsc = tb[lane];
             pnxt = tb[lane + 1].y;
         }
+        if constexpr (NAR) {
+            asm volatile("" ::: "memory");   // (issued after the descriptor loads)
+            nh = bin_nhdr_load(a.nhdr);
+            nar = nh.z == 4u;
+        }
         const uint32_t j1 = nrun / NP;
         hi0 = __builtin_amdgcn_readlane(pdsc.y, j1);
-        if (adma) {
-            ppk = pdsc.y | ((pnxt - pdsc.y) / (16 / sizeof(VT))) << 16;
-            bin_dma_runs_asm(pdsc.x, ppk, w * j1 / NW, (w + 1) * j1 / NW, stage, raw, hi0 - cap);
-        } else {
-            bin_dma_runs_pf(pdsc, pnxt, w * j1 / NW, (w + 1) * j1 / NW, stage, raw, clampm ? hi0 - cap : 0u);
+        if (adma) ppk = pdsc.y | ((pnxt - pdsc.y) / (16 / sizeof(VT))) << 16;
+        if (!nar) {   // (a narrow round copies its whole u32 image below)
+            if (adma)
+                bin_dma_runs_asm(pdsc.x, ppk, w * j1 / NW, (w + 1) * j1 / NW, stage, raw, hi0 - cap);
+            else
+                bin_dma_runs_pf(pdsc, pnxt, w * j1 / NW, (w + 1) * j1 / NW, stage, raw, clampm ? hi0 - cap : 0u);
         }
     }
     if constexpr (NP > 1) {
-        if (clampm && threadIdx.x < 16 / sizeof(VT)) raw[cap + threadIdx.x] = VT(0);   // +0 bits
+        if (clampm && !nar && threadIdx.x < 16 / sizeof(VT)) raw[cap + threadIdx.x] = VT(0);   // +0 bits
     }
     // ordinary loads next (their wait is the barrier's vmcnt(0) anyway)
     const VT xi = live ? reinterpret_cast<const VT*>(a.xin)[i] : VT(0);
@@ -411,8 +478,38 @@ __global__ __launch_bounds__(SB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) :
             ip[q] = make_uint4(t4.x, t4.y, t4.z, t4.w);
         }
     }
+    if constexpr (NAR) {
+        if (!pf) {   // (one-pass kernels: after the x_i and invpos loads)
+            asm volatile("" ::: "memory");
+            nh = bin_nhdr_load(a.nhdr);
+            nar = nh.z == 4u;
+        }
+    }
     VT v[D + 1];
-    if constexpr (NP == 1) {
+    bool picked = false;
+    if constexpr (NAR) {
+        if (nar) {   // narrow round: the block's u32 image in one pass, values = base + offset
+            uint32_t* r32 = reinterpret_cast<uint32_t*>(raw);
+            const uint32_t* s32 = reinterpret_cast<const uint32_t*>(stage);
+            if (pf) {
+                const uint32_t pk32 = pdsc.y | ((pnxt - pdsc.y) / 4u) << 16;
+                bin_dma_runs_asm(pdsc.x, pk32, w * nrun / NW, (w + 1) * nrun / NW, s32, r32, 0u);
+            } else {
+                bin_dma_runs_asm_tb(tb, w * nrun / NW, (w + 1) * nrun / NW, s32, r32);
+            }
+            bin_dma_wait();
+            __syncthreads();
+            if (a.ts) t1 = __builtin_amdgcn_s_memrealtime();
+            const uint64_t base = (uint64_t)nh.x | (uint64_t)nh.y << 32;
+#pragma unroll
+            for (int t = 0; t < D; ++t) v[1 + t] = __longlong_as_double((long long)(base + r32[pos_of(t)]));
+            picked = true;
+            // (the rule, store and partial below are shared with the 8-byte path; a separate copy
+            // here measured slower in both kinds of round: narrow 44.5 against 42.5 us)
+        }
+    }
+    if (picked) {
+    } else if constexpr (NP == 1) {
         if (pol & kPolAsmDmaT) {
             bin_dma_runs_asm_tb(tb, w * nrun / NW, (w + 1) * nrun / NW, stage, raw);
             bin_dma_wait();
@@ -655,20 +752,7 @@ __global__ __launch_bounds__(SB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) :
             else
                 res = apply_rule_reg<D, T, WMSR>(a.rule, v);
         }
-        if (pol & kPolSc1X) {   // write-through: no dirty x lines left in L2 at the kernel boundary
-            const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-                reinterpret_cast<VT*>(a.xout) + (i - threadIdx.x), 0, (int)(SB * sizeof(VT)), 0x00020000);
-            if constexpr (sizeof(VT) == 8) {
-                using UV = unsigned int __attribute__((ext_vector_type(2)));
-                UV bits;
-                __builtin_memcpy(&bits, &res, 8);
-                __builtin_amdgcn_raw_buffer_store_b64(bits, rx, threadIdx.x * 8u, 0, 16);
-            } else {
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, res), rx, threadIdx.x * 4u, 0, 16);
-            }
-        } else {
-            reinterpret_cast<VT*>(a.xout)[i] = res;
-        }
+        bin_store_x<SB>(a, i, res, pol);
         if (si == kHonest) {
             mn = res;
             mx = res;
@@ -687,7 +771,9 @@ __global__ __launch_bounds__(SB, FAULTY && NP > 1 ? ACS_FAULTY_WPE_OF(T, WMSR) :
 struct BinGeom {
     uint32_t D, dp, SA, P, Q, levels, SR, R, K, PK, QR;
     uint32_t SB;    // receivers per phase-B block (BinnedPlan::SB)
-    uint32_t pad;   // tile lengths padded to 16 bytes: 2 (fp64) or 4 (fp32) elements
+    uint32_t pad;   // tile lengths padded to 16 bytes: 2 (fp64) or 4 (fp32, narrow fp64) elements
+    uint32_t npad_or;   // 1: tiles' starts carry the run's pad count in their low bits (not on narrow
+                        // plans, whose 8-byte rounds address the starts in units of 2 entries)
     uint32_t none1, none2;   // tile count of level 1 / 2: the key of an absent CSR column (kEllNone),
                              // which sorts past every tile and is skipped by every fill kernel
 };
@@ -857,7 +943,7 @@ __global__ __launch_bounds__(256) void k_bin_prefix(const uint32_t* __restrict__
     for (uint32_t j = 0; j < nrun; ++j) {
         const uint64_t key = bin_run_key(G, b, j);
         const uint32_t npad = plen[key] - (tl[key].y - tl[key].x);
-        tiles[(uint64_t)b * (nrun + 1) + j] = make_uint2(pstart[key] | npad, pre);
+        tiles[(uint64_t)b * (nrun + 1) + j] = make_uint2(pstart[key] | (G.npad_or ? npad : 0u), pre);
         pre += plen[key];
     }
     tiles[(uint64_t)b * (nrun + 1) + nrun] = make_uint2(0u, pre);
@@ -963,6 +1049,7 @@ void binned_free(BinnedPlan& p) {
     (void)hipFree(p.stage2);
     (void)hipFree(p.xtag);
     (void)hipFree(p.fix);
+    (void)hipFree(p.nhdr);
     p = BinnedPlan{};
 }
 
@@ -1034,7 +1121,7 @@ hipError_t tile_sort(const uint32_t* ell, uint64_t E, const BinGeom& G, int leve
 
 hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t NR, uint32_t d, uint32_t dp,
                         uint32_t sa, uint32_t sb, bool tagged, bool f32, hipStream_t s, bool var,
-                        const uint32_t* status, bool clean) {
+                        const uint32_t* status, bool clean, bool narrow) {
     if (var && f32) return hipErrorNotSupported;   // CSR plans: fp64
     // receiver blocks other than kBinSB: clean plans of a compiled (d, sb) pair only
     if (sb != kBinSB && (var || tagged || !clean)) return hipErrorInvalidValue;
@@ -1042,10 +1129,18 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
     uint32_t sr = 0;
     const uint32_t levels = binned_levels(N, NR, d, sa, sb, &sr);
     if (!levels) return hipErrorNotSupported;
+    // ACSIM_BIN_PACK: bit 0 (default 1; 0: u16 phase-A index stream), read below
+    const char* pack_env = getenv("ACSIM_BIN_PACK");
+    const uint32_t pack = pack_env ? (uint32_t)strtoul(pack_env, nullptr, 10) : 1u;
+    // narrow stage: clean one-level fp64 plans of d = 16 / 32 at the default
+    // receiver block with the packed phase-A stream; confirmed at the end (phase-B LDS bound, passes)
+    const bool nar_req = narrow && !f32 && !tagged && !var && clean && sb == kBinSB && levels == 1 && sa <= 16384 &&
+                         (pack & 1u) && (d == 16 || d == 32);
     BinGeom G{};
     G.D = d;
     G.dp = dp;
-    G.pad = f32 ? 4u : 2u;
+    G.pad = f32 || nar_req ? 4u : 2u;
+    G.npad_or = nar_req ? 0u : 1u;
     G.SA = sa;
     G.P = (uint32_t)((N + sa - 1) / sa);
     G.SB = sb;
@@ -1099,12 +1194,10 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
         e = hipGetLastError();
     }
     // 14-bit packed phase-A indices (fp64 plans with source blocks of at most 2^14 senders).
-    // ACSIM_BIN_PACK: bit 0 (default 1; 0: u16 stream).  Measured per kernel (rocprofv3, cfg4,
+    // ACSIM_BIN_PACK bit 0.  Measured per kernel (rocprofv3, cfg4,
     // profiles/r04_s8_pack_kernel_stats.csv): packed idxA 59.4 -> 53-54 us.  Packed phase-B
     // positions measured slower (62.5-63.0 against 61.7-61.8 us: the decode sits on phase B's
     // critical path) and were removed in round 5 (history: d8efbd1).
-    const char* pack_env = getenv("ACSIM_BIN_PACK");
-    const uint32_t pack = pack_env ? (uint32_t)strtoul(pack_env, nullptr, 10) : 1u;
     if (e == hipSuccess && sa <= 16384) {   // fp64 and fp32 (bit 2 of ACSIM_BIN_PACK: no longer needed)
         if (pack & 1u) {
             const uint64_t nb = (p.Ep1 + 511) / 512;
@@ -1266,6 +1359,18 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
         p.segs = (uint32_t)((mx + p.chunk - 1) / p.chunk);
         if (p.segs == 0) p.segs = 1;
     }
+    // narrow plans: every block's u32 image must fit the phase-B LDS of its instantiation (the
+    // one- or two-pass kernel's buffer, in u32 entries), and the 8-byte rounds take one or two passes
+    if (e == hipSuccess && nar_req && p.pkA && p.split <= 2) {
+        const uint32_t raw_u32 = p.split == 2 ? 2u * (d * sb / 2 + d * sb / 16 + 2u) : 2u * (d * sb + d * sb / 16);
+        std::vector<uint2> h(((uint64_t)p.nrun + 1) * G.Q);
+        e = hipMemcpy(h.data(), p.tiles, h.size() * sizeof(uint2), hipMemcpyDeviceToHost);
+        bool fits = e == hipSuccess;
+        for (uint32_t b = 0; fits && b < G.Q; ++b) fits = h[(uint64_t)b * (p.nrun + 1) + p.nrun].y <= raw_u32;
+        if (fits) e = hipMalloc(&p.nhdr, sizeof(uint4));
+        if (fits && e == hipSuccess) e = hipMemset(p.nhdr, 0, sizeof(uint4));   // width 0: an 8-byte round
+        p.narrow = fits && e == hipSuccess;
+    }
     if (e == hipSuccess && getenv("ACSIM_BIN_TS")) {   // diagnostic workgroup timestamps
         p.ts_a = (p.P + 7) / 8 * 8 * p.segs;
         p.ts_b = (p.Q + 7) / 8 * 8;
@@ -1370,6 +1475,35 @@ static hipError_t launch_gather_sb(const BinnedPlan& p, const RoundArgs& a, cons
     return hipErrorNotSupported;
 }
 
+// Narrow plans: clean, default receiver block, d = 16 / 32, one or two passes
+// in the 8-byte rounds (the 4-byte rounds take one).
+template <int D, int T>
+static hipError_t launch_gather_narrow(const BinnedPlan& p, const RoundArgs& a, const double* src, dim3 grid,
+                                       uint32_t Qc, uint32_t pol, hipStream_t s) {
+    if constexpr (D == 16 || D == 32) {
+        const bool w_ = a.rule == 4;
+#define ACS_NAR_LAUNCH(W_, NP_)                                                                                  \
+    hipLaunchKernelGGL((k_bin_gather<D, T, W_, false, double, NP_, false, false, (int)kBinSB, true>), grid,         \
+                       dim3(kBinSB), 0, s, a, src, p.invpos, p.tiles, p.nrun, p.Q, Qc, pol)
+        if (p.split == 1) {
+            if (w_)
+                ACS_NAR_LAUNCH(true, 1);
+            else
+                ACS_NAR_LAUNCH(false, 1);
+            return hipGetLastError();
+        }
+        if (p.split == 2) {
+            if (w_)
+                ACS_NAR_LAUNCH(true, 2);
+            else
+                ACS_NAR_LAUNCH(false, 2);
+            return hipGetLastError();
+        }
+#undef ACS_NAR_LAUNCH
+    }
+    return hipErrorNotSupported;
+}
+
 hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool clean, hipStream_t s,
                                const FinalizeArgs* fin, uint32_t phases, SrcSel sel) {
     const FinalizeArgs fa = fin ? *fin : FinalizeArgs{};
@@ -1381,6 +1515,10 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
     // partials), or the caller's [qlo, qhi)
     RoundArgs a = a0;
     a.ts = p.ts ? p.ts + 3ull * p.ts_a : nullptr;
+    // narrow plans: clean whole rounds only (the chunked partitioned sequence never builds one)
+    const bool nar = p.narrow && p.nhdr && clean && !p.var && sel.n == 0 && p.SB == kBinSB;
+    if (p.narrow && !nar) return hipErrorInvalidValue;
+    a.nhdr = nar ? p.nhdr : nullptr;
     // phase B writes a.partial[b] for each of its receiver blocks b < p.Q (and neutral pairs up to
     // a.nblk): partials sized for fewer blocks would be written past their slice
     if ((phases & 4u) && a.nblk < p.Q) return hipErrorInvalidValue;
@@ -1405,7 +1543,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
         if (phases & 1)
             hipLaunchKernelGGL(k_bin_scatter<float>, dim3((nsrc + 7) / 8 * 8 * p.segs), dim3(kBinA), p.SA * sizeof(float), s,
                                fsrc, p.idxA, p.aoff, st1, a.st, a.N, p.SA, p.segs, p.chunk, pol, fa, fin_on, sel, p.ts, a.eacc,
-                               p.pkA);
+                               p.pkA, nullptr);
         if (p.levels == 2) {
             float* st2 = reinterpret_cast<float*>(p.stage2);
             if (phases & 2)
@@ -1461,7 +1599,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
     if (phases & 1)
         hipLaunchKernelGGL(k_bin_scatter<double>, dim3((nsrc + 7) / 8 * 8 * p.segs), dim3(kBinA), p.SA * sizeof(double), s, src,
                            p.idxA, p.aoff, p.stage1, a.st, a.N, p.SA, p.segs, p.chunk, pol, fa, fin_on, sel, p.ts, a.eacc,
-                           p.pkA);
+                           p.pkA, nar ? p.nhdr : nullptr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const double* last = p.stage1;
@@ -1481,6 +1619,7 @@ hipError_t launch_round_binned(const BinnedPlan& p, const RoundArgs& a0, bool cl
     const dim3 grid(8 * Qc);
 #define X(DD, TT)                                                                                        \
     if (p.D == DD && a.trim == TT) {                                                                     \
+        if (nar) return launch_gather_narrow<DD, TT>(p, a, last, grid, Qc, pol, s);                      \
         if (p.SB != kBinSB) return launch_gather_sb<DD, TT, double>(p, a, last, grid, Qc, pol, s);       \
         const bool w_ = a.rule == 4;                                                                     \
         if (p.var && clean && w_)                                                                        \
