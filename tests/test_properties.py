@@ -349,6 +349,68 @@ def test_gpu_binned_block_size_random_configs(oracle_mod, case):
 
 
 @st.composite
+def narrow_cases(draw):
+    """Opt-in narrow plans (ACSIM_BIN_NARROW=1): clean one-level fp64 plans of
+    d = 16 / 32 and every rule with a compiled (d, t) pair, FIXED runs long enough to reach the
+    4-byte rounds or EPS to a tight ε, one or two phase-B passes in the 8-byte rounds, initial
+    values shifted by draw (positive, negative, straddling zero, tiny).  -> (cfg, SA, passes, shift)"""
+    d = draw(st.sampled_from([16, 32]))
+    t = draw(st.sampled_from([5, 0]))
+    rule = draw(st.sampled_from(["trimmed", "midpoint", "dlpsw", "wmsr"] if t else ["average", "midpoint"]))
+    term = draw(st.sampled_from(["fixed", "fixed", "eps"]))
+    cfg = Config(n_nodes=draw(st.integers(3000, 90000)), topology="random_regular", degree=d, rule=rule, trim=t,
+                 eps=draw(st.sampled_from([1e-11, 1e-13])), max_rounds=draw(st.integers(30, 70)),
+                 termination=term, seed=draw(st.integers(0, 2 ** 40)), trace_spread=True)
+    return (cfg, draw(st.sampled_from([512, 1024, 2048, 4096, 16384])), draw(st.sampled_from(["", "1", "2"])),
+            draw(st.sampled_from(["none", "none", "negative", "straddle", "tiny"])))
+
+
+@pytest.mark.gpu
+@settings(max_examples=120, deadline=None, derandomize=True, database=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+@given(case=narrow_cases())
+def test_gpu_narrow_random_configs(oracle_mod, case):
+    """Narrow plans against the oracle bit for bit: rounds, spread trace, final values (every
+    round, whatever stage width it took)."""
+    import os
+    import acsim
+    cfg, sa, split, shift = case
+    env = {"ACSIM_BIN_NARROW": "1", "ACSIM_BIN_SA": str(sa), "ACSIM_BIN_SPLIT": split}
+    old = {k: os.environ.get(k) for k in env}
+    for k, v in env.items():
+        if v:
+            os.environ[k] = v
+        else:
+            os.environ.pop(k, None)
+    try:
+        with acsim.Simulator(cfg, device=0) as g:
+            name = g.kernel_name()
+            x0 = g.values(0).copy()
+            state = None
+            if shift != "none":
+                x = {"negative": -1.5 - x0, "straddle": x0 - 0.5, "tiny": x0 * 1e-300}[shift]
+                state = (0, x[None, :])
+                g.set_state(*state)
+            g.run()
+            gr, gt, gx = g.rounds(), g.spread_trace(0), g.values(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert "k_bin_" in name, (cfg, sa, name)
+    with oracle_mod.OracleSimulator(cfg.replace(omp_threads=16)) as o:
+        if state is not None:
+            o.set_state(*state)
+        o.run()
+        orr, ot, ox = o.rounds(), o.spread_trace(0), o.values(0)
+    assert np.array_equal(gr, orr), (cfg, sa, split, shift, name)
+    assert np.array_equal(_bits(gt), _bits(ot)), (cfg, sa, split, shift, name)
+    assert np.array_equal(_bits(gx), _bits(ox)), (cfg, sa, split, shift, name)
+
+
+@st.composite
 def partition_cases(draw):
     """Node-partitioned runs (SURVEY §8(e), cfg5's data flow) on virtual partitions: a binned or
     per-lane config, 2-8 row blocks, the chunked or the all-gather exchange, small source blocks."""
