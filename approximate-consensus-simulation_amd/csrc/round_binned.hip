@@ -1334,10 +1334,14 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
             if (fits) p.split = np;
         }
     }
-    // phase-A segmentation: for few source blocks about 256 workgroups per launch (one generation: one 128 KiB-LDS
-    // workgroup per CU, each x block staged once per CU; measured 66-68 -> 64 us fp64, 40-42 -> 39.4
-    // us fp32 on cfg4 against 512), a multiple of the 4096-position super-step, covering the
-    // longest block
+    // phase-A segmentation: for few source blocks one generation of workgroups per launch, a
+    // multiple of the 4096-position super-step, covering the longest block.  A generation is 256
+    // workgroups times the x images that fit a CU's 160 KiB of LDS together, at most 2: fp64
+    // source blocks (128 KiB) take one per CU, each x block staged once per CU (measured 66-68 ->
+    // 64 us against 512 workgroups on cfg4); fp32 ones (64 KiB) two, so that one stages its x block
+    // while the other streams (round 6, profiles/r06_fp32_awg_ab.json: phase A 40.0 -> 33.7 us on
+    // cfg4_f32 at 512 workgroups; 384 and 768 slower, as round 1 had measured 512 before the
+    // packed stream)
     if (e == hipSuccess) {
         std::vector<uint64_t> h((uint64_t)G.P + 1);
         e = hipMemcpy(h.data(), p.aoff, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost);
@@ -1346,7 +1350,9 @@ hipError_t binned_build(BinnedPlan& p, const uint32_t* ell, uint64_t N, uint64_t
         // With more source blocks than CUs (cfg5-sized graphs: several generations anyway), shorter
         // workgroups of about 48 Ki deliveries measured faster: cfg5 phase A 2525 -> 2085 us at 6
         // segments per block (profiles/r01_s38_cfg5_awg.txt).
-        uint64_t want = (256 + G.P - 1) / G.P;
+        const uint64_t fit = (160ull * 1024) / ((uint64_t)sa * (f32 ? 4 : 8) + 1024);
+        const uint64_t gen = 256 * (fit >= 2 ? 2 : 1);
+        uint64_t want = (gen + G.P - 1) / G.P;
         if (G.P > 256) want = (mx + 49151) / 49152;
         if (const char* v = getenv("ACSIM_BIN_AWG")) {   // phase-A workgroups per launch (sweeps)
             const uint64_t awg = strtoull(v, nullptr, 10);
